@@ -1,0 +1,398 @@
+#!/usr/bin/env python3
+"""bench.py — ec_encode_data throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "C2"): Reed-Solomon encode, k=10 sources,
+p=4 parity (ISA-L rows=4, m=14), Vandermonde matrix from gf_gen_rs_matrix,
+1 MiB shards, 1024 stripes per GPU, shards resident in HBM before timing.
+One step = one batched launch that encodes all 1024 stripes
+(isal_hip_batch_encode -> ec_encode_v16<4>).
+
+value = (k+p) * shard_bytes * stripes * steps * n_gpus / wall seconds, GiB/s
+        (the reference's perf_print byte convention, erasure_code_perf.c:304).
+
+Multi-GPU: one process per GPU (torchrun), stripes partitioned across ranks
+(weak scaling: every rank encodes its own 1024 stripes from its own HBM); RCCL
+carries only the control plane (broadcast of the coefficient matrix, barrier,
+max-reduce of timings). There is no data-path collective.
+
+Extra JSON fields:
+  roofline      dominant kernel's algorithmic bytes per launch / its average
+                launch duration (HIP events on the launch stream) vs 8 TB/s;
+  cpu_baseline  the reference's own CPU path (oracle/_ref/libisal_ref.so =
+                /root/reference erasure_code/ec_base.c built for this box's
+                host; nasm is absent so the AVX-512/GFNI kernels cannot be
+                assembled) on a bounded sample, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "isa-l_amd"))
+
+METRIC = "ec_encode_data GiB/s device-resident, k=10 m=4 1 MiB shards; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+GIB = float(1 << 30)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--p", type=int, default=4)
+    ap.add_argument("--len", type=int, default=1 << 20, help="shard bytes")
+    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU per step")
+    ap.add_argument("--workload", choices=["encode", "decode", "update"], default="encode")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all cores of this rank (<=16)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="exercise the distributed harness without a GPU (gloo, dummy step)")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# distributed harness (shared by the real and the dry-run path)
+# ---------------------------------------------------------------------------
+
+class Dist:
+    def __init__(self, dry: bool):
+        self.rank = int(os.environ.get("RANK", 0))
+        self.world = int(os.environ.get("WORLD_SIZE", 1))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", 0))
+        self.dist = None
+        self.backend = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            self.backend = "gloo" if dry else "nccl"  # nccl == RCCL on ROCm
+            dist.init_process_group(self.backend)
+            self.dist = dist
+
+    def _dev(self):
+        import torch
+
+        return torch.device("cpu") if self.backend == "gloo" else torch.device("cuda", self.local_rank)
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def broadcast_bytes(self, data: bytes) -> bytes:
+        """Control plane: rank 0's bytes to every rank (RCCL broadcast)."""
+        if not self.dist:
+            return data
+        import torch
+
+        t = torch.tensor(list(data), dtype=torch.uint8, device=self._dev())
+        self.dist.broadcast(t, src=0)
+        return bytes(t.cpu().tolist())
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64, device=self._dev())
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64, device=self._dev())
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed_steps(d: Dist, step, sync, steps: int, warmup: int):
+    """W untimed steps, then exactly K steps between barrier+sync brackets.
+    Returns the max over ranks of the wall time of the K steps."""
+    for _ in range(warmup):
+        step()
+    sync()
+    d.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    t1 = time.perf_counter()
+    d.barrier()
+    return d.max(t1 - t0)
+
+
+def control_plane_matrix(d: Dist, k: int, p: int) -> bytes:
+    """Rank 0 generates the m x k generator (gf_gen_rs_matrix) and broadcasts it."""
+    import isal_amd
+
+    a = isal_amd.gf_gen_rs_matrix(k + p, k).tobytes() if d.rank == 0 else bytes((k + p) * k)
+    return d.broadcast_bytes(a)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference's own ec_encode_data on this host
+# ---------------------------------------------------------------------------
+
+def cpu_baseline(k, p, n, seconds, threads, check=None):
+    """Times the reference ec_encode_data (oracle/_ref/libisal_ref.so: ec_base.c +
+    ec_base_aliases.c compiled from /root/reference) on `threads` host threads,
+    each encoding its own k x n stripe repeatedly for ~`seconds`.
+
+    check = (data_host[k][n], parity_gpu[p][n]): parity of that stripe recomputed
+    by the reference on the CPU must equal the GPU's bytes."""
+    import numpy as np
+
+    ref = os.path.join(REPO, "oracle", "_ref", "libisal_ref.so")
+    kind = "reference"
+    if not os.path.exists(ref):
+        ref, kind = os.path.join(REPO, "oracle", "liboracle.so"), "port"
+    if not os.path.exists(ref):
+        return None
+    L = ctypes.CDLL(ref)
+    prefix = "" if kind == "reference" else "oracle_"
+    enc = getattr(L, prefix + "ec_encode_data")
+    init = getattr(L, prefix + "ec_init_tables")
+    gen = getattr(L, prefix + "gf_gen_rs_matrix")
+    u8p = ctypes.POINTER(ctypes.c_ubyte)
+    enc.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.POINTER(u8p), ctypes.POINTER(u8p)]
+    enc.restype = None
+
+    a = np.zeros((k + p) * k, np.uint8)
+    gen(a.ctypes.data_as(u8p), k + p, k)
+    tbls = np.zeros(32 * k * p, np.uint8)
+    init(k, p, a[k * k:].ctypes.data_as(u8p), tbls.ctypes.data_as(u8p))
+
+    def ptrs(bufs):
+        arr = (u8p * len(bufs))()
+        for i, b in enumerate(bufs):
+            arr[i] = b.ctypes.data_as(u8p)
+        return arr
+
+    parity_ok = None
+    if check is not None:
+        data_h, parity_gpu = check
+        out = [np.zeros(n, np.uint8) for _ in range(p)]
+        enc(n, k, p, tbls.ctypes.data_as(u8p), ptrs(list(data_h)), ptrs(out))
+        parity_ok = all(np.array_equal(out[l], parity_gpu[l]) for l in range(p))
+
+    counts = [0] * threads
+    rng = np.random.default_rng(1)
+    bufs = [([rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)],
+             [np.zeros(n, np.uint8) for _ in range(p)]) for _ in range(threads)]
+    deadline = time.perf_counter() + seconds
+
+    def worker(i):
+        src, dst = ptrs(bufs[i][0]), ptrs(bufs[i][1])
+        t = tbls.ctypes.data_as(u8p)
+        while time.perf_counter() < deadline:
+            enc(n, k, p, t, src, dst)  # ctypes drops the GIL for the call
+            counts[i] += 1
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    wall = time.perf_counter() - t0
+    stripes = sum(counts)
+    return {
+        "value": round(stripes * (k + p) * n / wall / GIB, 4),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": f"{stripes} stripes of k={k} p={p} x {n} B, ec_encode_data from "
+                  f"{'reference ec_base.c (noarch; no nasm for the AVX-512/GFNI kernels)' if kind == 'reference' else 'oracle port of ec_base.c'}"
+                  f", {threads} threads x {wall:.1f} s",
+        "parity_stripe_match": parity_ok,
+    }
+
+
+# ---------------------------------------------------------------------------
+# main
+# ---------------------------------------------------------------------------
+
+def main(argv=None):
+    args = parse_args(argv)
+    d = Dist(args.dry_run)
+    if args.dry_run:
+        return dry_run(args, d)
+
+    import numpy as np
+    import torch
+
+    import isal_amd
+
+    torch.cuda.set_device(d.local_rank)
+    dev = torch.device("cuda", d.local_rank)
+    k, p, n, S = args.k, args.p, args.len, args.stripes
+    a = np.frombuffer(control_plane_matrix(d, k, p), dtype=np.uint8)
+
+    # shards resident in HBM: data[s][j], coding[s][l]
+    data = torch.empty((S, k, n), dtype=torch.uint8, device=dev)
+    data.random_(generator=torch.Generator(device=dev).manual_seed(1234 + d.rank))
+    dptr = [int(data[s, j].data_ptr()) for s in range(S) for j in range(k)]
+
+    if args.workload == "decode":
+        # C3: recover data shards {4,6,7} of every stripe from the k survivors
+        errs = [4, 6, 7]
+        rows = len(errs)
+        in_err = set(errs)
+        surv = [i for i in range(k + p) if i not in in_err][:k]
+        b = np.concatenate([a[r * k:(r + 1) * k] for r in surv])
+        ret, dinv, _ = isal_amd.gf_invert_matrix(b, k)
+        assert ret == 0
+        c = np.zeros(rows * k, np.uint8)
+        for i, e in enumerate(errs):
+            for j in range(k):
+                acc = 0
+                for r in range(k):
+                    acc ^= isal_amd.gf_mul(int(dinv[k * r + j]), int(a[k * e + r]))
+                c[k * i + j] = acc
+        coding = torch.empty((S, p, n), dtype=torch.uint8, device=dev)
+        enc = isal_amd.Batch(n, k, p, isal_amd.ec_init_tables(k, p, a[k * k:]), S, dptr,
+                             [int(coding[s, l].data_ptr()) for s in range(S) for l in range(p)])
+        enc.encode(torch.cuda.current_stream().cuda_stream)
+        frag = lambda s, i: data[s, i] if i < k else coding[s, i - k]  # noqa: E731
+        out = torch.empty((S, rows, n), dtype=torch.uint8, device=dev)
+        batch = isal_amd.Batch(n, k, rows, isal_amd.ec_init_tables(k, rows, c), S,
+                               [int(frag(s, i).data_ptr()) for s in range(S) for i in surv],
+                               [int(out[s, i].data_ptr()) for s in range(S) for i in range(rows)])
+        bytes_per_launch = (k + rows) * n * S
+        kernel = f"ec_encode_v16<{rows}>"
+        workload = f"C3 decode: recover data shards {errs} of k={k} p={p} RS, {n} B shards x {S} stripes/GPU"
+    else:
+        rows = p
+        out = torch.zeros((S, p, n), dtype=torch.uint8, device=dev)
+        batch = isal_amd.Batch(n, k, p, isal_amd.ec_init_tables(k, p, a[k * k:]), S, dptr,
+                               [int(out[s, l].data_ptr()) for s in range(S) for l in range(p)])
+        if args.workload == "encode":
+            bytes_per_launch = (k + p) * n * S
+            kernel = f"ec_encode_v16<{p}>"
+            workload = f"C2 encode: k={k} p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU"
+        else:
+            bytes_per_launch = (1 + 2 * p) * n * S
+            kernel = f"ec_update_v16<{p}>"
+            workload = (f"ec_encode_data_update: fold one source into p={p} parity (k={k}), "
+                        f"{n} B shards x {S} stripes/GPU, device-resident")
+
+    stream = torch.cuda.current_stream(dev)
+    h = stream.cuda_stream
+    vec = [0]
+
+    def step():
+        if args.workload == "update":
+            batch.update(vec[0] % k, h)
+            vec[0] += 1
+        else:
+            batch.encode(h)
+
+    # HIP events on the launch stream bracket exactly the K timed launches
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    d.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    d.barrier()
+    wall = d.max(t1 - t0)
+    launch_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+
+    if args.workload == "update":
+        step_bytes = (1 + 2 * p) * n * S
+    elif args.workload == "decode":
+        step_bytes = (k + rows) * n * S  # erasure_code_perf.c:324 convention
+    else:
+        step_bytes = (k + p) * n * S  # erasure_code_perf.c:304 convention
+    total = step_bytes * args.steps * d.world
+    value = total / wall / GIB
+    achieved = bytes_per_launch / launch_s / 1e9
+
+    result = {
+        "metric": METRIC if args.workload == "encode" else f"{args.workload} GiB/s device-resident",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": d.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (uniform random bytes, torch RNG on device)",
+        "config": {
+            "workload": workload,
+            "k": k, "p": p, "shard_bytes": n, "stripes_per_gpu": S,
+            "parallelism": f"stripes sharded over {d.world} GPU(s), no data-path collective",
+        },
+        "payload_gib_s": round(k * n * S * args.steps * d.world / wall / GIB, 2),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": kernel,
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "launch_ms": round(launch_s * 1e3, 4),
+            "bytes_per_launch": bytes_per_launch,
+        },
+    }
+    traffic = os.environ.get("ISAL_BENCH_TRAFFIC_BYTES")  # from the committed PMC pass
+    if traffic:
+        result["roofline"]["traffic"] = int(float(traffic))
+
+    if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        check = None
+        if args.workload == "encode":
+            check = (data[0].cpu().numpy(), out[0].cpu().numpy())
+        result["cpu_baseline"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check)
+    else:
+        result["cpu_baseline"] = None
+    if d.rank == 0:
+        print(json.dumps(result), flush=True)
+    d.close()
+    return 0
+
+
+def dry_run(args, d: Dist):
+    """Harness only (CPU, gloo): control-plane broadcast, barrier, max-over-ranks."""
+    import numpy as np
+
+    k, p = args.k, args.p
+    a = control_plane_matrix(d, k, p) if d.rank == 0 or d.world > 1 else b""
+    sleep = 0.002 * (1 + d.rank)
+    wall = timed_steps(d, lambda: time.sleep(sleep), lambda: None, args.steps, args.warmup)
+    total_stripes = d.sum(float(args.stripes))
+    if d.rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": d.world,
+                          "wall": wall, "stripes": total_stripes,
+                          "matrix_fnv": int(np.frombuffer(a, np.uint8).sum())}), flush=True)
+    d.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

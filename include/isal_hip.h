@@ -1,0 +1,72 @@
+/*
+ * isal_hip.h — MI355X-native extensions of the erasure-code engine.
+ *
+ * The reference API (erasure_code.h) is one synchronous call per stripe. On a
+ * GPU that shape is launch- and sync-bound, so the engine adds a batched,
+ * stream-ordered "stripe batch": nstripes independent stripes that share one
+ * coefficient matrix are encoded by ONE kernel launch over device-resident
+ * shards. This is additive: nothing in erasure_code.h depends on it, and the
+ * results of a batch are byte-identical to calling ec_encode_data /
+ * ec_encode_data_update once per stripe.
+ *
+ * All functions return 0 on success and a negative ISAL_HIP_E* code on error
+ * (they never abort). Streams are hipStream_t passed as void* so that this
+ * header needs no HIP include; NULL means the legacy default stream.
+ */
+#ifndef ISAL_HIP_ISAL_HIP_H
+#define ISAL_HIP_ISAL_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ISAL_HIP_OK 0
+#define ISAL_HIP_EINVAL (-1)   /* bad argument (size, count, NULL, unaligned pointer) */
+#define ISAL_HIP_EHIP (-2)     /* a HIP runtime call failed */
+#define ISAL_HIP_ENOMEM (-3)   /* host or device allocation failed */
+
+typedef struct isal_hip_batch isal_hip_batch;
+
+/*
+ * Describe a batch of stripes. len bytes per shard, k sources, rows outputs.
+ * gftbls: 32*k*rows bytes from ec_init_tables (host memory; copied).
+ * data:   host array of nstripes*k DEVICE pointers, stripe-major
+ *         (data[s*k + j] = shard j of stripe s).
+ * coding: host array of nstripes*rows DEVICE pointers (coding[s*rows + l]).
+ * Pointer tables and derived coefficient tables are uploaded once here; the
+ * launch functions below only enqueue kernels.
+ */
+int isal_hip_batch_create(isal_hip_batch **out, int len, int k, int rows,
+                          const unsigned char *gftbls, int nstripes, unsigned char *const *data,
+                          unsigned char *const *coding);
+
+/* Replace the coefficient tables (e.g. a decode matrix) of an existing batch. */
+int isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls);
+
+/* Enqueue ec_encode_data for every stripe of the batch on stream. */
+int isal_hip_batch_encode(isal_hip_batch *b, void *stream);
+
+/* Enqueue ec_encode_data_update(vec_i) for every stripe: source shard
+ * data[s*k + vec_i] is folded into coding[s*rows + l] for all l. */
+int isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream);
+
+int isal_hip_batch_destroy(isal_hip_batch *b);
+
+/* ---- introspection (tests, benchmarks) --------------------------------- */
+
+/* Number of erasure-code kernels this process has launched through the engine. */
+unsigned long long isal_hip_kernel_launches(void);
+
+/* Maximum parity rows one kernel pass produces (larger rows are split into passes). */
+int isal_hip_max_rows_per_pass(void);
+
+/* Name of the compiled GPU target ("gfx950"). */
+const char *isal_hip_target(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ISAL_HIP_ISAL_HIP_H */

@@ -1,0 +1,57 @@
+/*
+ * isal_hip_internal.h — contract between the C host shim (isal_hip_shim.c,
+ * gf_host.c) and the HIP kernel launchers (ec_kernels.hip). Not installed.
+ *
+ * Device argument layout (one contiguous device allocation per call or batch):
+ *
+ *   ptrs : uint64_t[nstripes][ptr_stride]   shard device addresses; for a
+ *          stripe s, sources at [s][src_idx0 + j], outputs at [s][dst_idx0 + l]
+ *   tbl  : uint32_t coefficient tables, grouped by row pass g (rows r0..r0+P-1,
+ *          P <= EC_MAX_ROWS_PER_PASS): group g starts at dword 5*k*r0 and is
+ *          laid out [j < k][l < P][5], so one source's tables for every output
+ *          of the pass are contiguous (one scalar-load burst per source).
+ *
+ * The 5 dwords of one coefficient c are three v_perm_b32 byte-lookup tables
+ * (GF(2^8) multiplication is GF(2)-linear, so c*x = c*(x&7) ^ c*(x&0x38) ^ c*(x&0xc0)):
+ *   [0],[1]  c*{0,1,..,7}             (entries 0-3 in [0], 4-7 in [1])
+ *   [2],[3]  c*{0,8,16,..,56}
+ *   [4]      c*{0,64,128,192}
+ */
+#ifndef ISAL_HIP_INTERNAL_H
+#define ISAL_HIP_INTERNAL_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EC_MAX_ROWS_PER_PASS 8
+#define EC_TBL_DWORDS 5
+
+/* Host GF math (gf_host.c). */
+unsigned char isal_hip_gf_mul(unsigned char a, unsigned char b);
+/* Fill the grouped perm tables above from 32-byte-per-coefficient gftbls
+ * (only byte 1 of each 32 B entry, the coefficient itself, is read — exactly
+ * what ec_base.c reads, so any gftbls gives the reference's answer). */
+void isal_hip_build_tables(int k, int rows, const unsigned char *gftbls, uint32_t *tbl);
+size_t isal_hip_tables_dwords(int k, int rows);
+
+/* Kernel launchers (ec_kernels.hip). Return 0 or a hipError_t value.
+ * `stream` is a hipStream_t. `vec16` = every shard address is 16-byte aligned. */
+int isal_hip_launch_encode(const uint64_t *d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
+                           const uint32_t *d_tbl, int len, int k, int rows, long long nstripes,
+                           int vec16, void *stream);
+int isal_hip_launch_update(const uint64_t *d_ptrs, int ptr_stride, int src_idx, int dst_idx0,
+                           const uint32_t *d_tbl, int len, int k, int rows, int vec_i,
+                           long long nstripes, int vec16, void *stream);
+
+/* Launch counter shared by the shim and the launchers. */
+void isal_hip_count_launch(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ISAL_HIP_INTERNAL_H */

@@ -1,0 +1,516 @@
+/*
+ * isal_hip_shim.c — the C-ABI boundary of the MI355X erasure-code engine.
+ *
+ * Exports the reference's data-path symbols (erasure_code.h, gf_vect_mul.h:
+ * ec_encode_data, ec_encode_data_update, gf_vect_dot_prod, gf_vect_mad,
+ * gf_vect_mul and their *_base twins) and the batched extension (isal_hip.h).
+ * Replaces the reference's L2 dispatch + L3 glue (ec_multibinary.asm:79-93,
+ * ec_highlevel_func.c:159-698): instead of picking a CPU ISA, every call is
+ * routed to the GPU kernels in ec_kernels.hip.
+ *
+ * Per call:
+ *   1. classify every shard pointer (device/managed vs host) with
+ *      hipPointerGetAttributes;
+ *   2. stage host-resident shards through a per-thread HBM scratch buffer,
+ *      in column chunks (so any len fits);
+ *   3. upload the stripe's pointer table + derived coefficient tables
+ *      (isal_hip_internal.h layout) from a per-thread pinned buffer;
+ *   4. launch, copy host-resident outputs back, synchronise — the reference
+ *      API is synchronous and results must be visible on return.
+ *
+ * There is no CPU compute path: a HIP failure prints the failing call and
+ * aborts (the reference API has no error return to carry it).
+ * Thread safety: all mutable state is per thread (pthread key) except the
+ * atomic launch counter.
+ */
+#include <hip/hip_runtime_api.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "erasure_code.h"
+#include "isal_hip.h"
+#include "isal_hip_internal.h"
+
+/* ---- errors ------------------------------------------------------------- */
+
+static void
+die(const char *what, hipError_t e)
+{
+        fprintf(stderr, "isal_hip: %s failed: %s (%d); no CPU fallback exists, aborting\n", what,
+                hipGetErrorString(e), (int) e);
+        abort();
+}
+
+#define HIP_OR_DIE(call)                                                                           \
+        do {                                                                                       \
+                hipError_t e_ = (call);                                                            \
+                if (e_ != hipSuccess)                                                              \
+                        die(#call, e_);                                                            \
+        } while (0)
+
+static unsigned long long g_launches;
+
+void
+isal_hip_count_launch(void)
+{
+        __atomic_add_fetch(&g_launches, 1ull, __ATOMIC_RELAXED);
+}
+
+unsigned long long
+isal_hip_kernel_launches(void)
+{
+        return __atomic_load_n(&g_launches, __ATOMIC_RELAXED);
+}
+
+int
+isal_hip_max_rows_per_pass(void)
+{
+        return EC_MAX_ROWS_PER_PASS;
+}
+
+const char *
+isal_hip_target(void)
+{
+        return "gfx950";
+}
+
+/* ---- per-thread context ------------------------------------------------- */
+
+/* Host-resident shards are staged through HBM in chunks of at most this many
+ * bytes in total (override: ISAL_HIP_STAGE_MB). */
+#define DEFAULT_STAGE_BYTES (256u << 20)
+
+typedef struct {
+        int device;
+        hipStream_t stream;
+        void *d_args; /* device: pointer table + coefficient tables */
+        void *h_args; /* pinned mirror of d_args */
+        size_t args_cap;
+        unsigned char *d_stage; /* device scratch for host-resident shards */
+        size_t stage_cap;
+} ctx_t;
+
+static pthread_key_t ctx_key;
+static pthread_once_t ctx_once = PTHREAD_ONCE_INIT;
+
+static void
+ctx_release(void *p)
+{
+        ctx_t *c = (ctx_t *) p;
+        if (!c)
+                return;
+        /* Best effort at thread exit: the runtime may already be shutting down. */
+        if (c->stream)
+                (void) hipStreamDestroy(c->stream);
+        if (c->d_args)
+                (void) hipFree(c->d_args);
+        if (c->h_args)
+                (void) hipHostFree(c->h_args);
+        if (c->d_stage)
+                (void) hipFree(c->d_stage);
+        free(c);
+}
+
+static void
+ctx_key_init(void)
+{
+        if (pthread_key_create(&ctx_key, ctx_release) != 0) {
+                fprintf(stderr, "isal_hip: pthread_key_create failed\n");
+                abort();
+        }
+}
+
+static ctx_t *
+ctx_get(void)
+{
+        ctx_t *c;
+        int dev;
+        pthread_once(&ctx_once, ctx_key_init);
+        HIP_OR_DIE(hipGetDevice(&dev));
+        c = (ctx_t *) pthread_getspecific(ctx_key);
+        if (c && c->device != dev) {
+                ctx_release(c);
+                c = NULL;
+        }
+        if (!c) {
+                c = (ctx_t *) calloc(1, sizeof(*c));
+                if (!c) {
+                        fprintf(stderr, "isal_hip: out of host memory\n");
+                        abort();
+                }
+                c->device = dev;
+                HIP_OR_DIE(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+                pthread_setspecific(ctx_key, c);
+        }
+        return c;
+}
+
+static void
+ensure_args(ctx_t *c, size_t bytes)
+{
+        size_t cap;
+        if (bytes <= c->args_cap)
+                return;
+        cap = c->args_cap ? c->args_cap : 64 * 1024;
+        while (cap < bytes)
+                cap *= 2;
+        if (c->d_args)
+                HIP_OR_DIE(hipFree(c->d_args));
+        if (c->h_args)
+                HIP_OR_DIE(hipHostFree(c->h_args));
+        c->d_args = c->h_args = NULL;
+        HIP_OR_DIE(hipMalloc(&c->d_args, cap));
+        HIP_OR_DIE(hipHostMalloc(&c->h_args, cap, hipHostMallocDefault));
+        c->args_cap = cap;
+}
+
+static void
+ensure_stage(ctx_t *c, size_t bytes)
+{
+        if (bytes <= c->stage_cap)
+                return;
+        if (c->d_stage)
+                HIP_OR_DIE(hipFree(c->d_stage));
+        c->d_stage = NULL;
+        HIP_OR_DIE(hipMalloc((void **) &c->d_stage, bytes));
+        c->stage_cap = bytes;
+}
+
+static size_t
+stage_limit(void)
+{
+        static size_t lim;
+        if (!lim) {
+                const char *e = getenv("ISAL_HIP_STAGE_MB");
+                size_t v = e ? (size_t) strtoull(e, NULL, 10) << 20 : 0;
+                lim = v ? v : DEFAULT_STAGE_BYTES;
+        }
+        return lim;
+}
+
+/* ---- pointer classification ------------------------------------------- */
+
+static int
+on_device(const void *p)
+{
+        hipPointerAttribute_t a;
+        hipError_t e;
+        if (!p)
+                return 0;
+        e = hipPointerGetAttributes(&a, p);
+        if (e != hipSuccess) {
+                (void) hipGetLastError(); /* unknown to HIP: plain host memory */
+                return 0;
+        }
+        return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+               a.type == hipMemoryTypeUnified;
+}
+
+/* ---- the generic synchronous call --------------------------------------- */
+
+enum { OP_ENCODE = 0, OP_UPDATE = 1 };
+
+/*
+ * OP_ENCODE: dst[l] = XOR_j c[l][j] * src[j], nsrc = k.
+ * OP_UPDATE: dst[l] ^= c[l][vec_i] * src[0], nsrc = 1.
+ */
+static void
+run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+       unsigned char *const *src, int nsrc, unsigned char *const *dst)
+{
+        ctx_t *c;
+        int nptr = nsrc + rows, i, nstage = 0;
+        int dev_flag[512];
+        int *flag;
+        size_t tbl_dwords, ptr_bytes, args_bytes, chunk, slot;
+        uint64_t *h_ptrs;
+        uint32_t *h_tbl;
+        long long c0;
+
+        if (len <= 0 || rows <= 0 || k < 0)
+                return;
+        if (op == OP_UPDATE && (vec_i < 0 || vec_i >= k)) {
+                /* Out-of-range vec_i is undefined in the reference (it reads past
+                 * gftbls); here it must not become an out-of-bounds GPU access. */
+                fprintf(stderr, "isal_hip: ec update with vec_i=%d outside [0,%d): ignored\n",
+                        vec_i, k);
+                return;
+        }
+        flag = nptr <= 512 ? dev_flag : (int *) malloc(sizeof(int) * (size_t) nptr);
+        if (!flag) {
+                fprintf(stderr, "isal_hip: out of host memory\n");
+                abort();
+        }
+        c = ctx_get();
+
+        for (i = 0; i < nptr; i++) {
+                const void *p = i < nsrc ? src[i] : dst[i - nsrc];
+                flag[i] = on_device(p);
+                nstage += !flag[i];
+        }
+
+        /* Column chunk: whole shard when nothing is staged. */
+        if (nstage) {
+                size_t per = stage_limit() / (size_t) nstage;
+                per &= ~(size_t) 4095;
+                if (per < 4096)
+                        per = 4096;
+                chunk = (size_t) len < per ? (size_t) len : per;
+                slot = (chunk + 255) & ~(size_t) 255; /* keep every slot 256-B aligned */
+                ensure_stage(c, slot * (size_t) nstage);
+        } else {
+                chunk = (size_t) len;
+                slot = 0;
+        }
+
+        tbl_dwords = isal_hip_tables_dwords(k, rows);
+        ptr_bytes = ((size_t) nptr * 8 + 15) & ~(size_t) 15;
+        args_bytes = ptr_bytes + tbl_dwords * 4;
+        ensure_args(c, args_bytes);
+        h_ptrs = (uint64_t *) c->h_args;
+        h_tbl = (uint32_t *) ((char *) c->h_args + ptr_bytes);
+        isal_hip_build_tables(k, rows, gftbls, h_tbl);
+
+        for (c0 = 0; c0 < len; c0 += (long long) chunk) {
+                int clen = (int) ((long long) len - c0 < (long long) chunk ? len - c0 : (long long) chunk);
+                int s = 0, vec16 = 1, err;
+                for (i = 0; i < nptr; i++) {
+                        unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
+                        uint64_t d;
+                        if (flag[i]) {
+                                d = (uint64_t) (uintptr_t) (host + c0);
+                        } else {
+                                unsigned char *st = c->d_stage + (size_t) s++ * slot;
+                                d = (uint64_t) (uintptr_t) st;
+                                /* sources, and outputs of a read-modify-write update, go in */
+                                if (i < nsrc || op == OP_UPDATE)
+                                        HIP_OR_DIE(hipMemcpyAsync(st, host + c0, (size_t) clen,
+                                                                  hipMemcpyHostToDevice, c->stream));
+                        }
+                        h_ptrs[i] = d;
+                        if (d & 15)
+                                vec16 = 0;
+                }
+                HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, args_bytes, hipMemcpyHostToDevice,
+                                          c->stream));
+                if (op == OP_ENCODE)
+                        err = isal_hip_launch_encode((const uint64_t *) c->d_args, nptr, 0, nsrc,
+                                                     (const uint32_t *) ((char *) c->d_args + ptr_bytes),
+                                                     clen, k, rows, 1, vec16, c->stream);
+                else
+                        err = isal_hip_launch_update((const uint64_t *) c->d_args, nptr, 0, nsrc,
+                                                     (const uint32_t *) ((char *) c->d_args + ptr_bytes),
+                                                     clen, k, rows, vec_i, 1, vec16, c->stream);
+                if (err)
+                        die("kernel launch", (hipError_t) err);
+                s = 0; /* staged slots are in pointer order: outputs follow sources */
+                for (i = 0; i < nptr; i++) {
+                        if (flag[i])
+                                continue;
+                        if (i >= nsrc)
+                                HIP_OR_DIE(hipMemcpyAsync(dst[i - nsrc] + c0,
+                                                          c->d_stage + (size_t) s * slot,
+                                                          (size_t) clen, hipMemcpyDeviceToHost,
+                                                          c->stream));
+                        s++;
+                }
+                HIP_OR_DIE(hipStreamSynchronize(c->stream));
+        }
+        if (flag != dev_flag)
+                free(flag);
+}
+
+/* ---- reference data-path ABI ------------------------------------------- */
+
+void
+ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
+               unsigned char **coding)
+{
+        run_ec(OP_ENCODE, len, k, rows, 0, gftbls, data, k, coding);
+}
+
+void
+ec_encode_data_base(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
+                    unsigned char **coding)
+{
+        run_ec(OP_ENCODE, len, k, rows, 0, gftbls, data, k, coding);
+}
+
+void
+ec_encode_data_update(int len, int k, int rows, int vec_i, unsigned char *gftbls,
+                      unsigned char *data, unsigned char **coding)
+{
+        run_ec(OP_UPDATE, len, k, rows, vec_i, gftbls, &data, 1, coding);
+}
+
+void
+ec_encode_data_update_base(int len, int k, int rows, int vec_i, unsigned char *gftbls,
+                           unsigned char *data, unsigned char **coding)
+{
+        run_ec(OP_UPDATE, len, k, rows, vec_i, gftbls, &data, 1, coding);
+}
+
+void
+gf_vect_dot_prod(int len, int vlen, unsigned char *gftbls, unsigned char **src,
+                 unsigned char *dest)
+{
+        run_ec(OP_ENCODE, len, vlen, 1, 0, gftbls, src, vlen, &dest);
+}
+
+void
+gf_vect_dot_prod_base(int len, int vlen, unsigned char *gftbls, unsigned char **src,
+                      unsigned char *dest)
+{
+        run_ec(OP_ENCODE, len, vlen, 1, 0, gftbls, src, vlen, &dest);
+}
+
+void
+gf_vect_mad(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src,
+            unsigned char *dest)
+{
+        run_ec(OP_UPDATE, len, vec, 1, vec_i, gftbls, &src, 1, &dest);
+}
+
+void
+gf_vect_mad_base(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src,
+                 unsigned char *dest)
+{
+        run_ec(OP_UPDATE, len, vec, 1, vec_i, gftbls, &src, 1, &dest);
+}
+
+/* dest = c * src with c = gftbl[1]; -1 (nothing touched) when len % 32 != 0,
+ * as ec_base.c:350-353. */
+int
+gf_vect_mul(int len, unsigned char *gftbl, void *src, void *dest)
+{
+        unsigned char *s = (unsigned char *) src, *d = (unsigned char *) dest;
+        if (len % 32)
+                return -1;
+        run_ec(OP_ENCODE, len, 1, 1, 0, gftbl, &s, 1, &d);
+        return 0;
+}
+
+int
+gf_vect_mul_base(int len, unsigned char *gftbl, unsigned char *src, unsigned char *dest)
+{
+        return gf_vect_mul(len, gftbl, src, dest);
+}
+
+/* ---- batched extension (isal_hip.h) ------------------------------------ */
+
+struct isal_hip_batch {
+        int len, k, rows, nstripes, device, vec16;
+        uint64_t *d_ptrs;
+        uint32_t *d_tbl;
+};
+
+int
+isal_hip_batch_create(isal_hip_batch **out, int len, int k, int rows, const unsigned char *gftbls,
+                      int nstripes, unsigned char *const *data, unsigned char *const *coding)
+{
+        isal_hip_batch *b;
+        uint64_t *h_ptrs;
+        long long s, stride = (long long) k + rows;
+        size_t nptr;
+        int j, vec16 = 1;
+        if (!out || len < 0 || k < 0 || rows <= 0 || nstripes <= 0 || !gftbls || !coding ||
+            (k > 0 && !data))
+                return ISAL_HIP_EINVAL;
+        *out = NULL;
+        b = (isal_hip_batch *) calloc(1, sizeof(*b));
+        nptr = (size_t) nstripes * (size_t) stride;
+        h_ptrs = (uint64_t *) malloc(nptr * 8);
+        if (!b || !h_ptrs) {
+                free(b);
+                free(h_ptrs);
+                return ISAL_HIP_ENOMEM;
+        }
+        for (s = 0; s < nstripes; s++) {
+                for (j = 0; j < k; j++)
+                        h_ptrs[s * stride + j] = (uint64_t) (uintptr_t) data[s * k + j];
+                for (j = 0; j < rows; j++)
+                        h_ptrs[s * stride + k + j] = (uint64_t) (uintptr_t) coding[s * rows + j];
+        }
+        for (s = 0; s < (long long) nptr; s++)
+                if (h_ptrs[s] & 15)
+                        vec16 = 0;
+        b->len = len;
+        b->k = k;
+        b->rows = rows;
+        b->nstripes = nstripes;
+        b->vec16 = vec16;
+        if (hipGetDevice(&b->device) != hipSuccess ||
+            hipMalloc((void **) &b->d_ptrs, nptr * 8) != hipSuccess ||
+            hipMemcpy(b->d_ptrs, h_ptrs, nptr * 8, hipMemcpyHostToDevice) != hipSuccess) {
+                free(h_ptrs);
+                isal_hip_batch_destroy(b);
+                return ISAL_HIP_EHIP;
+        }
+        free(h_ptrs);
+        if (isal_hip_batch_set_tables(b, gftbls) != 0) {
+                isal_hip_batch_destroy(b);
+                return ISAL_HIP_EHIP;
+        }
+        *out = b;
+        return ISAL_HIP_OK;
+}
+
+int
+isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
+{
+        size_t n;
+        uint32_t *h;
+        hipError_t e;
+        if (!b || !gftbls)
+                return ISAL_HIP_EINVAL;
+        n = isal_hip_tables_dwords(b->k, b->rows);
+        h = (uint32_t *) malloc(n * 4 + 4);
+        if (!h)
+                return ISAL_HIP_ENOMEM;
+        isal_hip_build_tables(b->k, b->rows, gftbls, h);
+        if (!b->d_tbl && hipMalloc((void **) &b->d_tbl, n * 4 + 4) != hipSuccess) {
+                free(h);
+                return ISAL_HIP_EHIP;
+        }
+        e = hipMemcpy(b->d_tbl, h, n * 4, hipMemcpyHostToDevice);
+        free(h);
+        return e == hipSuccess ? ISAL_HIP_OK : ISAL_HIP_EHIP;
+}
+
+int
+isal_hip_batch_encode(isal_hip_batch *b, void *stream)
+{
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        return isal_hip_launch_encode(b->d_ptrs, b->k + b->rows, 0, b->k, b->d_tbl, b->len, b->k,
+                                      b->rows, b->nstripes, b->vec16, stream)
+                       ? ISAL_HIP_EHIP
+                       : ISAL_HIP_OK;
+}
+
+int
+isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream)
+{
+        if (!b || vec_i < 0 || vec_i >= b->k)
+                return ISAL_HIP_EINVAL;
+        return isal_hip_launch_update(b->d_ptrs, b->k + b->rows, vec_i, b->k, b->d_tbl, b->len,
+                                      b->k, b->rows, vec_i, b->nstripes, b->vec16, stream)
+                       ? ISAL_HIP_EHIP
+                       : ISAL_HIP_OK;
+}
+
+int
+isal_hip_batch_destroy(isal_hip_batch *b)
+{
+        if (!b)
+                return ISAL_HIP_OK;
+        if (b->d_ptrs)
+                (void) hipFree(b->d_ptrs);
+        if (b->d_tbl)
+                (void) hipFree(b->d_tbl);
+        free(b);
+        return ISAL_HIP_OK;
+}

@@ -1,0 +1,275 @@
+"""isal_amd — Python mirror of the reference erasure-code API over libisal_hip.so.
+
+The product is the C-ABI library ``isa-l_amd/lib/libisal_hip.so`` (headers in
+``include/``). This module binds it with ctypes, keeping the reference's
+function names, argument order and meaning (reference include/erasure_code.h,
+include/gf_vect_mul.h), so tests and the benchmark read like the reference's
+own C tests. Buffers may be numpy uint8 arrays (host memory), torch tensors
+(host or device; their storage address is passed), or raw integer addresses.
+
+There is no fallback: importing works without a GPU (host-side functions such
+as gf_mul or ec_init_tables need none), but every data-path call goes to the
+GPU through the library, and a missing library raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Sequence
+
+import numpy as np
+
+__all__ = [
+    "LIB_PATH", "lib", "gf_mul", "gf_inv", "gf_gen_rs_matrix", "gf_gen_cauchy1_matrix",
+    "gf_invert_matrix", "gf_vect_mul_init", "ec_init_tables", "ec_encode_data",
+    "ec_encode_data_base", "ec_encode_data_update", "ec_encode_data_update_base",
+    "gf_vect_dot_prod", "gf_vect_dot_prod_base", "gf_vect_mad", "gf_vect_mad_base",
+    "gf_vect_mul", "gf_vect_mul_base", "Batch", "kernel_launches", "max_rows_per_pass",
+    "version", "addr",
+]
+
+LIB_PATH = os.environ.get(
+    "ISAL_HIP_LIB",
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), os.pardir, "lib", "libisal_hip.so"),
+)
+
+_u8p = ctypes.POINTER(ctypes.c_ubyte)
+_u8pp = ctypes.POINTER(_u8p)
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libisal_hip.so (raises if it has not been built: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        path = os.path.abspath(LIB_PATH)
+        if not os.path.exists(path):
+            raise RuntimeError(f"libisal_hip.so not built at {path}: run `make -C isa-l_amd`")
+        L = ctypes.CDLL(path)
+        i, v = ctypes.c_int, None
+        sig = {
+            "gf_mul": (ctypes.c_ubyte, [ctypes.c_ubyte, ctypes.c_ubyte]),
+            "gf_inv": (ctypes.c_ubyte, [ctypes.c_ubyte]),
+            "gf_gen_rs_matrix": (v, [_u8p, i, i]),
+            "gf_gen_cauchy1_matrix": (v, [_u8p, i, i]),
+            "gf_invert_matrix": (i, [_u8p, _u8p, i]),
+            "gf_vect_mul_init": (v, [ctypes.c_ubyte, _u8p]),
+            "gf_vect_mul_init_base": (v, [ctypes.c_ubyte, _u8p]),
+            "ec_init_tables": (v, [i, i, _u8p, _u8p]),
+            "ec_init_tables_base": (v, [i, i, _u8p, _u8p]),
+            "ec_encode_data": (v, [i, i, i, _u8p, _u8pp, _u8pp]),
+            "ec_encode_data_base": (v, [i, i, i, _u8p, _u8pp, _u8pp]),
+            "ec_encode_data_update": (v, [i, i, i, i, _u8p, _u8p, _u8pp]),
+            "ec_encode_data_update_base": (v, [i, i, i, i, _u8p, _u8p, _u8pp]),
+            "gf_vect_dot_prod": (v, [i, i, _u8p, _u8pp, _u8p]),
+            "gf_vect_dot_prod_base": (v, [i, i, _u8p, _u8pp, _u8p]),
+            "gf_vect_mad": (v, [i, i, i, _u8p, _u8p, _u8p]),
+            "gf_vect_mad_base": (v, [i, i, i, _u8p, _u8p, _u8p]),
+            "gf_vect_mul": (i, [i, _u8p, ctypes.c_void_p, ctypes.c_void_p]),
+            "gf_vect_mul_base": (i, [i, _u8p, _u8p, _u8p]),
+            "isal_get_version": (ctypes.c_uint, []),
+            "isal_get_version_str": (ctypes.c_char_p, []),
+            "isal_hip_batch_create": (i, [ctypes.POINTER(ctypes.c_void_p), i, i, i, _u8p, i, _u8pp, _u8pp]),
+            "isal_hip_batch_set_tables": (i, [ctypes.c_void_p, _u8p]),
+            "isal_hip_batch_encode": (i, [ctypes.c_void_p, ctypes.c_void_p]),
+            "isal_hip_batch_update": (i, [ctypes.c_void_p, i, ctypes.c_void_p]),
+            "isal_hip_batch_destroy": (i, [ctypes.c_void_p]),
+            "isal_hip_kernel_launches": (ctypes.c_ulonglong, []),
+            "isal_hip_max_rows_per_pass": (i, []),
+            "isal_hip_target": (ctypes.c_char_p, []),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+# ---------------------------------------------------------------------------
+# buffer plumbing
+# ---------------------------------------------------------------------------
+
+def addr(buf) -> int:
+    """Address of a byte buffer: numpy array, torch tensor, ctypes buffer or int."""
+    if isinstance(buf, int):
+        return buf
+    if isinstance(buf, np.ndarray):
+        if not buf.flags["C_CONTIGUOUS"]:
+            raise ValueError("buffer must be C-contiguous")
+        return buf.ctypes.data
+    if hasattr(buf, "data_ptr"):  # torch.Tensor
+        if not buf.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return int(buf.data_ptr())
+    if isinstance(buf, (ctypes.Array, bytearray)):
+        return ctypes.addressof(ctypes.c_char.from_buffer(buf))
+    raise TypeError(f"unsupported buffer type {type(buf)!r}")
+
+
+def _p(buf) -> _u8p:
+    return ctypes.cast(ctypes.c_void_p(addr(buf)), _u8p)
+
+
+def _pp(bufs: Sequence) -> ctypes.Array:
+    arr = (_u8p * max(1, len(bufs)))()
+    for j, b in enumerate(bufs):
+        arr[j] = _p(b)
+    return arr
+
+
+def _u8(a) -> np.ndarray:
+    a = np.ascontiguousarray(np.frombuffer(bytes(a), dtype=np.uint8) if isinstance(a, (bytes, bytearray)) else a,
+                             dtype=np.uint8)
+    return a
+
+
+# ---------------------------------------------------------------------------
+# host-side GF math (reference ec_base.c:37-280 semantics)
+# ---------------------------------------------------------------------------
+
+def gf_mul(a: int, b: int) -> int:
+    return int(lib().gf_mul(a & 0xFF, b & 0xFF))
+
+
+def gf_inv(a: int) -> int:
+    return int(lib().gf_inv(a & 0xFF))
+
+
+def gf_gen_rs_matrix(m: int, k: int) -> np.ndarray:
+    a = np.zeros(m * k, dtype=np.uint8)
+    lib().gf_gen_rs_matrix(_p(a), m, k)
+    return a
+
+
+def gf_gen_cauchy1_matrix(m: int, k: int) -> np.ndarray:
+    a = np.zeros(m * k, dtype=np.uint8)
+    lib().gf_gen_cauchy1_matrix(_p(a), m, k)
+    return a
+
+
+def gf_invert_matrix(mat, n: int):
+    """Returns (ret, inverse, destroyed_input) like the C call (input is copied first)."""
+    inp = _u8(mat).copy()
+    out = np.zeros(n * n, dtype=np.uint8)
+    ret = lib().gf_invert_matrix(_p(inp), _p(out), n)
+    return int(ret), out, inp
+
+
+def gf_vect_mul_init(c: int) -> np.ndarray:
+    t = np.zeros(32, dtype=np.uint8)
+    lib().gf_vect_mul_init(c & 0xFF, _p(t))
+    return t
+
+
+def ec_init_tables(k: int, rows: int, a) -> np.ndarray:
+    a = _u8(a)
+    t = np.zeros(max(1, 32 * k * rows), dtype=np.uint8)
+    lib().ec_init_tables(k, rows, _p(a), _p(t))
+    return t
+
+
+# ---------------------------------------------------------------------------
+# data path (GPU) — same argument order as the C API
+# ---------------------------------------------------------------------------
+
+def ec_encode_data(len_: int, k: int, rows: int, gftbls, data: Sequence, coding: Sequence) -> None:
+    lib().ec_encode_data(len_, k, rows, _p(gftbls), _pp(data), _pp(coding))
+
+
+def ec_encode_data_base(len_: int, k: int, rows: int, gftbls, data: Sequence, coding: Sequence) -> None:
+    lib().ec_encode_data_base(len_, k, rows, _p(gftbls), _pp(data), _pp(coding))
+
+
+def ec_encode_data_update(len_: int, k: int, rows: int, vec_i: int, gftbls, data, coding: Sequence) -> None:
+    lib().ec_encode_data_update(len_, k, rows, vec_i, _p(gftbls), _p(data), _pp(coding))
+
+
+def ec_encode_data_update_base(len_: int, k: int, rows: int, vec_i: int, gftbls, data, coding: Sequence) -> None:
+    lib().ec_encode_data_update_base(len_, k, rows, vec_i, _p(gftbls), _p(data), _pp(coding))
+
+
+def gf_vect_dot_prod(len_: int, vlen: int, gftbls, src: Sequence, dest) -> None:
+    lib().gf_vect_dot_prod(len_, vlen, _p(gftbls), _pp(src), _p(dest))
+
+
+def gf_vect_dot_prod_base(len_: int, vlen: int, gftbls, src: Sequence, dest) -> None:
+    lib().gf_vect_dot_prod_base(len_, vlen, _p(gftbls), _pp(src), _p(dest))
+
+
+def gf_vect_mad(len_: int, vec: int, vec_i: int, gftbls, src, dest) -> None:
+    lib().gf_vect_mad(len_, vec, vec_i, _p(gftbls), _p(src), _p(dest))
+
+
+def gf_vect_mad_base(len_: int, vec: int, vec_i: int, gftbls, src, dest) -> None:
+    lib().gf_vect_mad_base(len_, vec, vec_i, _p(gftbls), _p(src), _p(dest))
+
+
+def gf_vect_mul(len_: int, gftbl, src, dest) -> int:
+    return int(lib().gf_vect_mul(len_, _p(gftbl), ctypes.c_void_p(addr(src)), ctypes.c_void_p(addr(dest))))
+
+
+def gf_vect_mul_base(len_: int, gftbl, src, dest) -> int:
+    return int(lib().gf_vect_mul_base(len_, _p(gftbl), _p(src), _p(dest)))
+
+
+# ---------------------------------------------------------------------------
+# batched extension (include/isal_hip.h)
+# ---------------------------------------------------------------------------
+
+class Batch:
+    """nstripes stripes sharing one coefficient matrix; shards are device buffers.
+
+    data[s*k + j] / coding[s*rows + l] are addresses (or tensors) of stripe s.
+    encode()/update() only enqueue on `stream` (a hipStream_t as int; 0 = default).
+    """
+
+    def __init__(self, len_: int, k: int, rows: int, gftbls, nstripes: int,
+                 data: Sequence, coding: Sequence):
+        self.len, self.k, self.rows, self.nstripes = len_, k, rows, nstripes
+        if len(data) != nstripes * k or len(coding) != nstripes * rows:
+            raise ValueError("pointer lists must hold nstripes*k and nstripes*rows entries")
+        h = ctypes.c_void_p()
+        rc = lib().isal_hip_batch_create(ctypes.byref(h), len_, k, rows, _p(gftbls), nstripes,
+                                         _pp(data), _pp(coding))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_create failed ({rc})")
+        self._h = h
+
+    def set_tables(self, gftbls) -> None:
+        rc = lib().isal_hip_batch_set_tables(self._h, _p(gftbls))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_set_tables failed ({rc})")
+
+    def encode(self, stream: int = 0) -> None:
+        rc = lib().isal_hip_batch_encode(self._h, ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_encode failed ({rc})")
+
+    def update(self, vec_i: int, stream: int = 0) -> None:
+        rc = lib().isal_hip_batch_update(self._h, vec_i, ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_update failed ({rc})")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().isal_hip_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def kernel_launches() -> int:
+    return int(lib().isal_hip_kernel_launches())
+
+
+def max_rows_per_pass() -> int:
+    return int(lib().isal_hip_max_rows_per_pass())
+
+
+def version() -> str:
+    return lib().isal_get_version_str().decode()

@@ -1,0 +1,36 @@
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import ecutil  # noqa: E402
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libisal_hip.so on the GPU)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    return ecutil.oracle()
+
+
+@pytest.fixture(scope="session")
+def engine():
+    """The product library (isa-l_amd/lib/libisal_hip.so) through its Python mirror."""
+    ecutil.build_engine()
+    import isal_amd
+
+    isal_amd.lib()
+    return isal_amd
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """Fails (does not skip) when the GPU is missing: -m gpu runs must not pass vacuously."""
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    return torch.device("cuda:0")
