@@ -38,6 +38,22 @@ _u8pp = ctypes.POINTER(_u8p)
 _lib = None
 
 
+def _one_hip_runtime() -> None:
+    """A process must hold exactly ONE HIP runtime. PyTorch-ROCm ships its own
+    libamdhip64.so.7; if libisal_hip.so were loaded first it would bind
+    /opt/rocm's copy, torch would then load a second one, and whichever
+    initialises second sees no device. Loading torch first makes the engine's
+    NEEDED libamdhip64.so.7 resolve to the runtime torch already holds (same
+    SONAME), so device pointers and streams are shared. Set ISAL_AMD_NO_TORCH=1
+    in processes that never use torch."""
+    if os.environ.get("ISAL_AMD_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> ctypes.CDLL:
     """Load libisal_hip.so (raises if it has not been built: no silent fallback)."""
     global _lib
@@ -45,6 +61,7 @@ def lib() -> ctypes.CDLL:
         path = os.path.abspath(LIB_PATH)
         if not os.path.exists(path):
             raise RuntimeError(f"libisal_hip.so not built at {path}: run `make -C isa-l_amd`")
+        _one_hip_runtime()
         L = ctypes.CDLL(path)
         i, v = ctypes.c_int, None
         sig = {

@@ -3,6 +3,9 @@ import sys
 
 import pytest
 
+# Exactly one HIP runtime per process: torch's (see isal_amd._one_hip_runtime).
+import torch  # noqa: F401,E402
+
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import ecutil  # noqa: E402
