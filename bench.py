@@ -74,7 +74,15 @@ class Dist:
             import torch.distributed as dist
 
             self.backend = "gloo" if dry else "nccl"  # nccl == RCCL on ROCm
-            dist.init_process_group(self.backend)
+            if dry:
+                dist.init_process_group(self.backend)
+            else:
+                import torch
+
+                # bind this rank's GPU first so RCCL builds its communicator on it
+                torch.cuda.set_device(self.local_rank)
+                dist.init_process_group(self.backend,
+                                        device_id=torch.device("cuda", self.local_rank))
             self.dist = dist
 
     def _dev(self):
@@ -136,12 +144,51 @@ def timed_steps(d: Dist, step, sync, steps: int, warmup: int):
     return d.max(t1 - t0)
 
 
+def enc_group(k: int) -> int:
+    """Sources per load group the engine launches with (ec_kernels.hip:enc_group)."""
+    return next((u for u in (12, 10, 8, 6, 5, 4) if k >= u and k % u == 0), 4)
+
+
 def control_plane_matrix(d: Dist, k: int, p: int) -> bytes:
     """Rank 0 generates the m x k generator (gf_gen_rs_matrix) and broadcasts it."""
     import isal_amd
 
     a = isal_amd.gf_gen_rs_matrix(k + p, k).tobytes() if d.rank == 0 else bytes((k + p) * k)
     return d.broadcast_bytes(a)
+
+
+# ---------------------------------------------------------------------------
+# HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes
+# ---------------------------------------------------------------------------
+
+def pmc_traffic(workload, k, p, n, S, kernel):
+    """HBM bytes per launch measured by `rocprofv3 --pmc FETCH_SIZE` and
+    `--pmc WRITE_SIZE` (separate passes) of this same bench configuration,
+    committed under profiles/*_pmc_*.csv. gfx950 correction: FETCH_SIZE counts
+    half of a wide streaming read, so bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB.
+    Returns (bytes, source) for the newest matching file, or None."""
+    import glob
+    import statistics
+
+    want = {"workload": workload, "k": str(k), "p": str(p), "len": str(n), "stripes": str(S)}
+    name = kernel.split("<")[0] + "<" + kernel.split("<")[1].split(">")[0].split(",")[0]
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_*.csv")), reverse=True):
+        with open(path) as f:
+            lines = f.read().splitlines()
+        cfg = next((l for l in lines if l.startswith("# config:")), "")
+        kv = dict(t.split("=", 1) for t in cfg[len("# config:"):].split(";")[0].split() if "=" in t)
+        if any(kv.get(a) != b for a, b in want.items()):
+            continue
+        vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+        for l in lines:
+            parts = l.split(",")
+            if len(parts) >= 4 and parts[0] in vals and parts[3].replace(" ", "").startswith(
+                    "void" + name.replace(" ", "")):
+                vals[parts[0]].append(float(parts[2]))
+        if vals["FETCH_SIZE"] and vals["WRITE_SIZE"]:
+            kib = 2 * statistics.median(vals["FETCH_SIZE"]) + statistics.median(vals["WRITE_SIZE"])
+            return int(kib * 1024), os.path.relpath(path, REPO)
+    return None
 
 
 # ---------------------------------------------------------------------------
@@ -272,7 +319,7 @@ def main(argv=None):
                                [int(frag(s, i).data_ptr()) for s in range(S) for i in surv],
                                [int(out[s, i].data_ptr()) for s in range(S) for i in range(rows)])
         bytes_per_launch = (k + rows) * n * S
-        kernel = f"ec_encode_v16<{rows}>"
+        kernel = f"ec_encode_v16<{rows}, EncNT<{enc_group(k)}>>"
         workload = f"C3 decode: recover data shards {errs} of k={k} p={p} RS, {n} B shards x {S} stripes/GPU"
     else:
         rows = p
@@ -281,7 +328,7 @@ def main(argv=None):
                                [int(out[s, l].data_ptr()) for s in range(S) for l in range(p)])
         if args.workload == "encode":
             bytes_per_launch = (k + p) * n * S
-            kernel = f"ec_encode_v16<{p}>"
+            kernel = f"ec_encode_v16<{p}, EncNT<{enc_group(k)}>>"
             workload = f"C2 encode: k={k} p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU"
         else:
             bytes_per_launch = (1 + 2 * p) * n * S
@@ -359,9 +406,10 @@ def main(argv=None):
             "bytes_per_launch": bytes_per_launch,
         },
     }
-    traffic = os.environ.get("ISAL_BENCH_TRAFFIC_BYTES")  # from the committed PMC pass
+    traffic = pmc_traffic(args.workload, k, p, n, S, kernel)
     if traffic:
-        result["roofline"]["traffic"] = int(float(traffic))
+        result["roofline"]["traffic"] = traffic[0]
+        result["roofline"]["traffic_source"] = traffic[1]
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))

@@ -66,15 +66,40 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const u32x4 __attribute__((address_space(1)))* gload_t;
 typedef u32x4 __attribute__((address_space(1)))* gstore_t;
 
+template <bool NT = false>
 __device__ __forceinline__ uint4 load16(uint64_t base, long long off) {
-  const u32x4 v = *(gload_t)(base + off);
+  u32x4 v;
+  if constexpr (NT)
+    v = __builtin_nontemporal_load((gload_t)(base + off));
+  else
+    v = *(gload_t)(base + off);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+template <bool NT = false>
 __device__ __forceinline__ void store16(uint64_t base, long long off, uint4 v) {
   u32x4 w = {v.x, v.y, v.z, v.w};
-  *(gstore_t)(base + off) = w;
+  if constexpr (NT)
+    __builtin_nontemporal_store(w, (gstore_t)(base + off));
+  else
+    *(gstore_t)(base + off) = w;
 }
+
+// Tuning policy of the vector encode kernel (tools/ec_probe.hip explores others).
+//   U      sources whose loads are issued together before any arithmetic
+//   NT_LD  non-temporal source loads;  NT_ST  non-temporal parity stores
+//   ORDER  0: work item = (stripe, tile) with tile fastest; 1: stripe fastest
+// Measured on MI355X (profiles/r01_probe_variants_*.txt): non-temporal loads
+// AND stores lift the 10-read/4-write stream from 5.5 to 6.1 TB/s, and issuing
+// all of a stripe's source loads at once (U = k) adds ~1 %; the work order and
+// shard padding do not help. The library picks U from k at launch (enc_group).
+template <int UU>
+struct EncNT {
+  static constexpr int U = UU;
+  static constexpr bool NT_LD = true, NT_ST = true;
+  static constexpr int ORDER = 0;
+};
+using EncDefault = EncNT<4>;
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU op (gfx950)
@@ -126,18 +151,23 @@ __device__ __forceinline__ void mac16x2(uint32_t (&acc)[P][4], const uint4& x, c
 // U sources j..j+U-1: issue all U loads before any arithmetic, then fold the
 // sources in pairs; the scheduling barriers keep one pair's temporaries live
 // at a time (otherwise the scheduler hoists every lookup and spills).
-template <int P, int U>
+template <int P, int U, bool NT = false>
 __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
                                         int j, long long off, const uint32_t* __restrict__ tbl) {
   uint4 x[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) x[u] = load16(sp[j + u], off);
+  for (int u = 0; u < U; ++u) x[u] = load16<NT>(sp[j + u], off);
+  // Pairs share XOR3s but hold two sources' tables (2*P*5 SGPRs): only for P <= 4.
+  constexpr int PAIR = P <= 4 ? 2 : 1;
 #pragma unroll
-  for (int u = 0; u + 1 < U; u += 2) {
-    mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
+  for (int u = 0; u + PAIR <= U; u += PAIR) {
+    if constexpr (PAIR == 2)
+      mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
+    else
+      mac16<P>(acc, x[u], tbl + (j + u) * P * kTbl);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (U & 1) {
+  if constexpr (PAIR == 2 && (U & 1)) {
     mac16<P>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -169,17 +199,36 @@ __device__ __forceinline__ void dot_bytes(const uint64_t* __restrict__ sp, int s
 // Work item w = (stripe, 4 KiB tile), tile fastest; grid-stride over items.
 // ---------------------------------------------------------------------------
 // Waves per SIMD the register allocator must allow (VGPR budget 512/waves).
-template <int P>
-constexpr int enc_waves() { return P <= 2 ? 8 : (P <= 4 ? 6 : 4); }
+// Live VGPRs ~ 4U (loads in flight) + 4P (accumulators) + ~32 (selectors,
+// table halves, addresses); the 512-entry file gives 512/alloc waves per SIMD.
+template <int P, int U>
+constexpr int enc_waves() {
+  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8;
+  constexpr int w = 512 / est;
+  return w > 8 ? 8 : (w < 4 ? 4 : w);
+}
 
-template <int P>
-__global__ __launch_bounds__(kBlock, enc_waves<P>()) void ec_encode_v16(const uint64_t* __restrict__ ptrs,
-                                                        int ptr_stride, int src0, int dst0,
-                                                        const uint32_t* __restrict__ tbl, int len,
-                                                        int k, unsigned nitems, unsigned tiles) {
+template <int P, class Pol = EncDefault>
+__global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U>())) void ec_encode_v16(
+    const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
+    const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles) {
+  const unsigned nstripes = nitems / tiles;
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
-    const unsigned stripe = w / tiles;
-    const unsigned tile = w - stripe * tiles;
+    unsigned stripe, tile;
+    if constexpr (Pol::ORDER == 0) {
+      stripe = w / tiles;
+      tile = w - stripe * tiles;
+    } else if constexpr (Pol::ORDER == 2) {
+      // XCD-contiguous: blocks b, b+8, b+16.. (one XCD under round-robin
+      // dispatch) walk one contiguous eighth of the items. Speed only.
+      const unsigned per = nitems >> 3;
+      const unsigned v = (nitems & 7) ? w : (w & 7) * per + (w >> 3);
+      stripe = v / tiles;
+      tile = v - stripe * tiles;
+    } else {
+      tile = w / nstripes;
+      stripe = w - tile * nstripes;
+    }
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
@@ -188,15 +237,19 @@ __global__ __launch_bounds__(kBlock, enc_waves<P>()) void ec_encode_v16(const ui
       for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
       const uint64_t* __restrict__ src = sp + src0;
       int j = 0;
-      for (; j + 4 <= k; j += 4) chunk16<P, 4>(acc, src, j, off, tbl);
-      if (j + 2 <= k) {
-        chunk16<P, 2>(acc, src, j, off, tbl);
-        j += 2;
+      for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::NT_LD>(acc, src, j, off, tbl);
+      // Remainder. The launcher only picks U > 4 when U divides k, so there the
+      // (cheap, correct for any k) single-source loop is dead in practice.
+      if constexpr (Pol::U == 4) {
+        if (j + 2 <= k) {
+          chunk16<P, 2, Pol::NT_LD>(acc, src, j, off, tbl);
+          j += 2;
+        }
       }
-      if (j < k) chunk16<P, 1>(acc, src, j, off, tbl);
+      for (; j < k; ++j) chunk16<P, 1, Pol::NT_LD>(acc, src, j, off, tbl);
 #pragma unroll
       for (int l = 0; l < P; ++l)
-        store16(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]));
+        store16<Pol::NT_ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]));
     } else if (off < len) {
       dot_bytes<P>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off));
     }
@@ -246,10 +299,10 @@ __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restri
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
-      const uint4 x = load16(sp[src_idx], off);
+      const uint4 x = load16<true>(sp[src_idx], off);
       uint4 d[P];
 #pragma unroll
-      for (int l = 0; l < P; ++l) d[l] = load16(sp[dst0 + l], off);
+      for (int l = 0; l < P; ++l) d[l] = load16<true>(sp[dst0 + l], off);
       const Sel s0 = split(x.x), s1 = split(x.y), s2 = split(x.z), s3 = split(x.w);
 #pragma unroll
       for (int l = 0; l < P; ++l) {
@@ -258,7 +311,7 @@ __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restri
         d[l].y ^= gf_mul4(c, s1);
         d[l].z ^= gf_mul4(c, s2);
         d[l].w ^= gf_mul4(c, s3);
-        store16(sp[dst0 + l], off, d[l]);
+        store16<true>(sp[dst0 + l], off, d[l]);
       }
     } else if (off < len) {
       mad_bytes<P>(sp, src_idx, dst0, tbl, off, static_cast<int>(len - off));
@@ -298,18 +351,42 @@ unsigned grid_for(unsigned nitems) {
   return (cap && nitems > cap) ? cap : nitems;
 }
 
+// Load-group size for k sources: the largest of {12,10,8,6,5,4} dividing k
+// (all of a stripe's loads in flight at once for the common k), else 4.
+int enc_group(int k) {
+  static const int cand[] = {12, 10, 8, 6, 5, 4};
+  for (int u : cand)
+    if (k >= u && k % u == 0) return u;
+  return 4;
+}
+
+template <int P, int U>
+void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
+                int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles) {
+  hipLaunchKernelGGL((ec_encode_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), 0, s, ptrs,
+                     ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
+}
+
 template <int P>
 hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0, const uint32_t* tbl,
                        int len, int k, unsigned nstripes, bool vec16, hipStream_t s) {
   const unsigned span = vec16 ? kTile : kBlock;
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
   const unsigned nitems = nstripes * tiles;
-  if (vec16)
-    hipLaunchKernelGGL(ec_encode_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
-                       ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
-  else
-    hipLaunchKernelGGL(ec_encode_b1<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
-                       ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
+  const unsigned grid = grid_for(nitems);
+  if (vec16) {
+    switch (enc_group(k)) {
+      case 12: launch_v16<P, 12>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
+      case 10: launch_v16<P, 10>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
+      case 8: launch_v16<P, 8>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
+      case 6: launch_v16<P, 6>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
+      case 5: launch_v16<P, 5>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
+      default: launch_v16<P, 4>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
+    }
+  } else {
+    hipLaunchKernelGGL(ec_encode_b1<P>, dim3(grid), dim3(kBlock), 0, s, ptrs, ptr_stride, src0,
+                       dst0, tbl, len, k, nitems, tiles);
+  }
   isal_hip_count_launch();
   return hipGetLastError();
 }

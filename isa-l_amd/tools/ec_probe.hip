@@ -1,0 +1,262 @@
+// ec_probe.hip — measurement tool, not part of libisal_hip.so.
+//
+// 1. Achievable HBM bandwidth for the encode access pattern: memory-only
+//    kernels with exactly the addressing of ec_encode_v16 (R source streams
+//    read, W parity streams written, XOR instead of GF math), plus a plain copy.
+// 2. Policy variants of the real encode kernel (EncDefault vs others), checked
+//    bit-exact against the default variant.
+// Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24);
+// median and min per variant. Output: one line per variant + a JSON summary.
+#include "../csrc/ec_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+extern "C" void gf_gen_rs_matrix(unsigned char* a, int m, int k);
+extern "C" void ec_init_tables(int k, int rows, unsigned char* a, unsigned char* gftbls);
+extern "C" void isal_hip_count_launch(void) {}
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+namespace {
+
+template <int R, int W, bool NT_LD, bool NT_ST>
+__global__ __launch_bounds__(256) void mem_pattern(const uint64_t* __restrict__ ptrs, int stride,
+                                                   int len, unsigned nitems, unsigned tiles,
+                                                   uint32_t* __restrict__ sink) {
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned stripe = w / tiles, tile = w - stripe * tiles;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * stride;
+    const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
+    uint4 a = make_uint4(w, 1, 2, 3);
+    uint4 x[R > 0 ? R : 1];
+#pragma unroll
+    for (int j = 0; j < R; ++j) x[j] = load16<NT_LD>(sp[j], off);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      a.x ^= x[j].x;
+      a.y ^= x[j].y;
+      a.z ^= x[j].z;
+      a.w ^= x[j].w;
+    }
+    if constexpr (W == 0) {
+      if ((a.x ^ a.y ^ a.z ^ a.w) == 0x9E3779B9u) sink[threadIdx.x] = a.x;
+    }
+#pragma unroll
+    for (int l = 0; l < W; ++l) {
+      store16<NT_ST>(sp[10 + l], off, a);  // parity pointers (k = 10) only
+      a.x += 1;
+    }
+  }
+}
+
+__global__ void copy16(const uint4* __restrict__ s, uint4* __restrict__ d, size_t n16) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16;
+       i += (size_t)gridDim.x * blockDim.x)
+    d[i] = s[i];
+}
+
+__global__ void fill_random(uint32_t* p, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = static_cast<uint32_t>(z ^ (z >> 31));
+  }
+}
+
+template <int UU, bool NL, bool NS, int ORD>
+struct Pol {
+  static constexpr int U = UU;
+  static constexpr bool NT_LD = NL, NT_ST = NS;
+  static constexpr int ORDER = ORD;
+};
+
+struct Variant {
+  std::string name;
+  double bytes;  // algorithmic bytes per launch
+  std::function<void(hipStream_t)> run;
+  std::vector<double> gbs;
+  bool encode = false;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int k = argc > 1 ? atoi(argv[1]) : 10;
+  const int p = argc > 2 ? atoi(argv[2]) : 4;
+  const int len = argc > 3 ? atoi(argv[3]) : (1 << 20);
+  const int S = argc > 4 ? atoi(argv[4]) : 1024;
+  const int rounds = argc > 5 ? atoi(argv[5]) : 5;
+  const int iters = 10;
+  if (k != 10 || p != 4) {
+    fprintf(stderr, "memory patterns are instantiated for k=10 p=4 only\n");
+    return 2;
+  }
+  const size_t shard = static_cast<size_t>(len);
+  const size_t maxpad = 65536 + 4096;
+  const size_t dbytes = shard * k * S, cbytes = shard * p * S;
+  const size_t dalloc = (shard + maxpad) * k * S, calloc_ = (shard + maxpad) * p * S;
+  uint8_t *data, *coding, *sinkp;
+  CK(hipMalloc(&data, dalloc));
+  CK(hipMalloc(&coding, calloc_));
+  CK(hipMalloc(&sinkp, 4096));
+  hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (uint32_t*)data, dalloc / 4, 7u);
+  CK(hipDeviceSynchronize());
+
+  // pointer table [S][k+p] and coefficient tables (C2 Vandermonde)
+  std::vector<uint64_t> h_ptrs(static_cast<size_t>(S) * (k + p));
+  for (int s = 0; s < S; ++s) {
+    for (int j = 0; j < k; ++j)
+      h_ptrs[(size_t)s * (k + p) + j] = (uint64_t)(data + ((size_t)s * k + j) * shard);
+    for (int l = 0; l < p; ++l)
+      h_ptrs[(size_t)s * (k + p) + k + l] = (uint64_t)(coding + ((size_t)s * p + l) * shard);
+  }
+  std::vector<unsigned char> a((k + p) * k), g(32 * k * p);
+  gf_gen_rs_matrix(a.data(), k + p, k);
+  ec_init_tables(k, p, a.data() + k * k, g.data());
+  std::vector<uint32_t> h_tbl(isal_hip_tables_dwords(k, p));
+  isal_hip_build_tables(k, p, g.data(), h_tbl.data());
+  uint64_t* d_ptrs;
+  uint32_t* d_tbl;
+  CK(hipMalloc(&d_ptrs, h_ptrs.size() * 8));
+  CK(hipMalloc(&d_tbl, h_tbl.size() * 4 + 4));
+  CK(hipMemcpy(d_ptrs, h_ptrs.data(), h_ptrs.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_tbl, h_tbl.data(), h_tbl.size() * 4, hipMemcpyHostToDevice));
+  // padded layouts: shard stride len + pad (partition-camping check)
+  const size_t pads[3] = {256, 4096, 65536 + 4096};
+  uint64_t* d_pptrs[3];
+  for (int q = 0; q < 3; ++q) {
+    std::vector<uint64_t> hp(h_ptrs.size());
+    const size_t st = shard + pads[q];
+    for (int s2 = 0; s2 < S; ++s2) {
+      for (int j = 0; j < k; ++j) hp[(size_t)s2 * (k + p) + j] = (uint64_t)(data + ((size_t)s2 * k + j) * st);
+      for (int l = 0; l < p; ++l)
+        hp[(size_t)s2 * (k + p) + k + l] = (uint64_t)(coding + ((size_t)s2 * p + l) * st);
+    }
+    CK(hipMalloc(&d_pptrs[q], hp.size() * 8));
+    CK(hipMemcpy(d_pptrs[q], hp.data(), hp.size() * 8, hipMemcpyHostToDevice));
+  }
+
+  const unsigned tiles = (len + kTile - 1) / kTile;
+  const unsigned nitems = S * tiles;
+  const int stride = k + p;
+  const double enc_bytes = (double)(k + p) * shard * S;
+  std::vector<Variant> V;
+
+#define PATTERN(R, W, NL, NS, NAME)                                                            \
+  V.push_back({NAME, (double)((R) + (W)) * shard * S, [=](hipStream_t st) {                     \
+                 hipLaunchKernelGGL((mem_pattern<R, W, NL, NS>), dim3(nitems), dim3(256), 0, st, \
+                                    d_ptrs, stride, len, nitems, tiles, (uint32_t*)sinkp);      \
+               }});
+  PATTERN(10, 4, false, false, "mem read10+write4")
+  PATTERN(10, 4, true, true, "mem read10+write4 nt/nt")
+  PATTERN(10, 4, false, true, "mem read10+write4 ld/nt")
+  PATTERN(10, 0, false, false, "mem read10 only")
+  PATTERN(0, 4, false, false, "mem write4 only")
+  // first half of the parity buffer copied onto its second half: cbytes moved
+  // (the source shards are never written, so encode outputs stay comparable)
+  V.push_back({"copy16 (1 read : 1 write)", (double)cbytes, [=](hipStream_t st) {
+                 hipLaunchKernelGGL(copy16, dim3(8192), dim3(256), 0, st, (const uint4*)coding,
+                                    (uint4*)(coding + cbytes / 2), cbytes / 2 / 16);
+               }});
+  V.push_back({"hipMemcpyDtoD 4 GiB", 2.0 * (double)cbytes, [=](hipStream_t st) {
+                 CK(hipMemcpyAsync(coding, data, cbytes, hipMemcpyDeviceToDevice, st));
+               }});
+
+#define ENC(POL, GRID, NAME)                                                                  \
+  V.push_back({NAME, enc_bytes, [=](hipStream_t st) {                                          \
+                 unsigned gr = (GRID) ? std::min<unsigned>((GRID), nitems) : nitems;          \
+                 hipLaunchKernelGGL((ec_encode_v16<4, POL>), dim3(gr), dim3(256), 0, st, d_ptrs, \
+                                    stride, 0, k, (const uint32_t*)d_tbl, len, k, nitems, tiles); \
+               }});                                                                           \
+  V.back().encode = true;
+  using PNB = Pol<4, true, true, 0>;
+  using PNB2 = Pol<2, true, true, 0>;
+  using PNB5 = Pol<5, true, true, 0>;
+  using PNB10 = Pol<10, true, true, 0>;
+  using PNBX = Pol<4, true, true, 2>;
+  using PNB10X = Pol<10, true, true, 2>;
+  using PX = Pol<4, false, false, 2>;
+  ENC(EncDefault, 0, "encode default (U4)")
+  ENC(PNB, 0, "encode U4 nt-both")
+  ENC(PNB2, 0, "encode U2 nt-both")
+  ENC(PNB5, 0, "encode U5 nt-both")
+  ENC(PNB10, 0, "encode U10 nt-both")
+  ENC(PNBX, 0, "encode U4 nt-both xcd-contig")
+  ENC(PNB10X, 0, "encode U10 nt-both xcd-contig")
+  ENC(PX, 0, "encode U4 xcd-contig")
+#define ENCP(POL, Q, NAME)                                                                     \
+  V.push_back({NAME, enc_bytes, [=](hipStream_t st) {                                          \
+                 hipLaunchKernelGGL((ec_encode_v16<4, POL>), dim3(nitems), dim3(256), 0, st,     \
+                                    d_pptrs[Q], stride, 0, k, (const uint32_t*)d_tbl, len, k,    \
+                                    nitems, tiles);                                            \
+               }});
+  ENCP(PNB, 0, "encode U4 nt-both pad256 (unchecked)")
+  ENCP(PNB, 1, "encode U4 nt-both pad4K (unchecked)")
+  ENCP(PNB, 2, "encode U4 nt-both pad68K (unchecked)")
+  ENCP(EncDefault, 1, "encode U4 pad4K (unchecked)")
+
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+
+  // reference parity from the default variant
+  std::vector<uint8_t> want(cbytes / S * 2), got(cbytes / S * 2);
+  auto grab = [&](std::vector<uint8_t>& out) {
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(out.data(), coding, cbytes / S, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(out.data() + cbytes / S, coding + cbytes - cbytes / S, cbytes / S,
+                 hipMemcpyDeviceToHost));
+  };
+  V[7].run(st);  // encode default
+  grab(want);
+
+  for (int r = 0; r < rounds; ++r) {
+    for (auto& v : V) {
+      v.run(st);  // warm
+      CK(hipEventRecord(e0, st));
+      for (int i = 0; i < iters; ++i) v.run(st);
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.gbs.push_back(v.bytes / (ms / iters * 1e-3) / 1e9);
+      if (v.encode) {
+        CK(hipMemsetAsync(coding, 0, cbytes / S, st));
+        v.run(st);
+        grab(got);
+        if (memcmp(got.data(), want.data(), want.size()) != 0) {
+          fprintf(stderr, "MISMATCH in variant %s\n", v.name.c_str());
+          return 3;
+        }
+      }
+    }
+  }
+  printf("%-34s %10s %10s %8s\n", "variant", "median", "max", "%8TB/s");
+  std::string json = "{";
+  for (auto& v : V) {
+    std::vector<double> s = v.gbs;
+    std::sort(s.begin(), s.end());
+    const double med = s[s.size() / 2], mx = s.back();
+    printf("%-34s %10.1f %10.1f %8.1f\n", v.name.c_str(), med, mx, med / 80.0);
+    json += "\"" + v.name + "\": " + std::to_string(med) + ", ";
+  }
+  json += "\"unit\": \"GB/s (algorithmic bytes / launch time, median of rounds)\"}";
+  printf("%s\n", json.c_str());
+  return 0;
+}
