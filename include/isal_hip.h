@@ -54,6 +54,37 @@ int isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream);
 
 int isal_hip_batch_destroy(isal_hip_batch *b);
 
+/* ---- streaming pipeline for HOST-resident stripes ----------------------- */
+
+/*
+ * Stripes whose shards live in host memory (NIC / disk buffers) flow through
+ * `depth` HBM slots on three HIP streams: host->device copies of the sources,
+ * GF arithmetic, device->host copies of the parity, overlapped across stripes.
+ *   ISAL_HIP_PIPE_UPDATE: each source is folded into the parity as soon as it
+ *                         lands (ec_encode_data_update semantics, parity
+ *                         starts zeroed);
+ *   ISAL_HIP_PIPE_ENCODE: one ec_encode_data launch once all k sources landed.
+ * Pinned host buffers give full copy/compute overlap; pageable ones work but
+ * serialise the copies.
+ */
+#define ISAL_HIP_PIPE_UPDATE 0
+#define ISAL_HIP_PIPE_ENCODE 1
+
+typedef struct isal_hip_pipe isal_hip_pipe;
+
+int isal_hip_pipe_create(isal_hip_pipe **out, int len, int k, int rows,
+                         const unsigned char *gftbls, int depth, int mode);
+
+/* Enqueue one stripe: data = k host source pointers, coding = rows host parity
+ * pointers (written when the stripe completes). Blocks only while all `depth`
+ * slots are busy. Buffers must stay valid until isal_hip_pipe_flush returns. */
+int isal_hip_pipe_submit(isal_hip_pipe *p, unsigned char *const *data, unsigned char *const *coding);
+
+/* Wait until every submitted stripe's parity is in host memory. */
+int isal_hip_pipe_flush(isal_hip_pipe *p);
+
+int isal_hip_pipe_destroy(isal_hip_pipe *p);
+
 /* ---- introspection (tests, benchmarks) --------------------------------- */
 
 /* Number of erasure-code kernels this process has launched through the engine. */

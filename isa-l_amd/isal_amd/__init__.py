@@ -24,7 +24,7 @@ __all__ = [
     "gf_invert_matrix", "gf_vect_mul_init", "ec_init_tables", "ec_encode_data",
     "ec_encode_data_base", "ec_encode_data_update", "ec_encode_data_update_base",
     "gf_vect_dot_prod", "gf_vect_dot_prod_base", "gf_vect_mad", "gf_vect_mad_base",
-    "gf_vect_mul", "gf_vect_mul_base", "Batch", "kernel_launches", "max_rows_per_pass",
+    "gf_vect_mul", "gf_vect_mul_base", "Batch", "Pipe", "kernel_launches", "max_rows_per_pass",
     "version", "addr",
 ]
 
@@ -91,6 +91,10 @@ def lib() -> ctypes.CDLL:
             "isal_hip_batch_encode": (i, [ctypes.c_void_p, ctypes.c_void_p]),
             "isal_hip_batch_update": (i, [ctypes.c_void_p, i, ctypes.c_void_p]),
             "isal_hip_batch_destroy": (i, [ctypes.c_void_p]),
+            "isal_hip_pipe_create": (i, [ctypes.POINTER(ctypes.c_void_p), i, i, i, _u8p, i, i]),
+            "isal_hip_pipe_submit": (i, [ctypes.c_void_p, _u8pp, _u8pp]),
+            "isal_hip_pipe_flush": (i, [ctypes.c_void_p]),
+            "isal_hip_pipe_destroy": (i, [ctypes.c_void_p]),
             "isal_hip_kernel_launches": (ctypes.c_ulonglong, []),
             "isal_hip_max_rows_per_pass": (i, []),
             "isal_hip_target": (ctypes.c_char_p, []),
@@ -271,6 +275,50 @@ class Batch:
     def close(self) -> None:
         if getattr(self, "_h", None):
             lib().isal_hip_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Pipe:
+    """Streaming encoder for host-resident stripes (include/isal_hip.h pipeline).
+
+    mode "update": sources folded into parity as they land (ec_encode_data_update);
+    mode "encode": one ec_encode_data per stripe once all sources landed.
+    Host buffers must stay alive until flush() returns."""
+
+    MODES = {"update": 0, "encode": 1}
+
+    def __init__(self, len_: int, k: int, rows: int, gftbls, depth: int = 3, mode: str = "update"):
+        self.len, self.k, self.rows = len_, k, rows
+        h = ctypes.c_void_p()
+        rc = lib().isal_hip_pipe_create(ctypes.byref(h), len_, k, rows, _p(gftbls), depth,
+                                        self.MODES[mode])
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_pipe_create failed ({rc})")
+        self._h = h
+        self._keep = []
+
+    def submit(self, data: Sequence, coding: Sequence) -> None:
+        d, c = _pp(data), _pp(coding)
+        self._keep.append((d, c))  # pointer arrays are read at submit; keep refs cheap anyway
+        rc = lib().isal_hip_pipe_submit(self._h, d, c)
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_pipe_submit failed ({rc})")
+
+    def flush(self) -> None:
+        rc = lib().isal_hip_pipe_flush(self._h)
+        self._keep.clear()
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_pipe_flush failed ({rc})")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().isal_hip_pipe_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -345,3 +345,30 @@ def test_reference_test_programs(name, gpu):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "Pass" in r.stdout or "pass" in r.stdout.lower()
+
+
+# --------------------------------------------------------------------------
+# host-memory streaming pipeline (isal_hip_pipe_*)
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("mode", ["update", "encode"])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_pipe_host_stripes_vs_oracle(engine, oracle, gpu, mode, pinned):
+    import torch
+
+    k, p, n, ns = 20, 6, 256 * 1024 + 48, 7
+    a = engine.gf_gen_rs_matrix(k + p, k)
+    tbls = engine.ec_init_tables(k, p, a[k * k:])
+    src = torch.from_numpy(np.stack([np.stack([fill_bytes(n, 1000 * s + j) for j in range(k)]) for s in range(ns)]))
+    par = torch.full((ns, p, n), 0xEE, dtype=torch.uint8)
+    if pinned:
+        src, par = src.pin_memory(), par.pin_memory()
+    pipe = engine.Pipe(n, k, p, tbls, depth=3, mode=mode)
+    for s in range(ns):
+        pipe.submit([src[s, j] for j in range(k)], [par[s, l] for l in range(p)])
+    pipe.flush()
+    pipe.close()
+    for s in range(ns):
+        want = oracle.encode(a[k * k:], k, p, [src[s, j].numpy() for j in range(k)])
+        for l in range(p):
+            assert np.array_equal(par[s, l].numpy(), want[l]), (mode, pinned, s, l)
