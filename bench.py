@@ -198,7 +198,7 @@ def pmc_traffic(workload, k, p, n, S, kernel):
 # CPU baseline: the reference's own ec_encode_data on this host
 # ---------------------------------------------------------------------------
 
-def cpu_baseline(k, p, n, seconds, threads, check=None):
+def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference"):
     """Times the reference ec_encode_data (oracle/_ref/libisal_ref.so: ec_base.c +
     ec_base_aliases.c compiled from /root/reference) on `threads` host threads,
     each encoding its own k x n stripe repeatedly for ~`seconds`.
@@ -207,17 +207,33 @@ def cpu_baseline(k, p, n, seconds, threads, check=None):
     by the reference on the CPU must equal the GPU's bytes."""
     import numpy as np
 
-    ref = os.path.join(REPO, "oracle", "_ref", "libisal_ref.so")
-    kind = "reference"
-    if not os.path.exists(ref):
-        ref, kind = os.path.join(REPO, "oracle", "liboracle.so"), "port"
-    if not os.path.exists(ref):
-        return None
-    L = ctypes.CDLL(ref)
-    prefix = "" if kind == "reference" else "oracle_"
-    enc = getattr(L, prefix + "ec_encode_data")
-    init = getattr(L, prefix + "ec_init_tables")
-    gen = getattr(L, prefix + "gf_gen_rs_matrix")
+    if impl == "gfni":
+        # port of the reference's AVX-512+GFNI kernels (oracle/ec_gfni_port.c);
+        # tables and matrix from the oracle restatement of ec_base.c
+        lib_path, kind = os.path.join(REPO, "oracle", "libgfni_port.so"), "port"
+        if not (os.path.exists(lib_path) and os.path.exists(os.path.join(REPO, "oracle", "liboracle.so"))):
+            return None
+        G = ctypes.CDLL(lib_path)
+        if not G.gfni_port_available():
+            return None
+        L = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+        enc = G.gfni_port_ec_encode_data
+        init, gen = L.oracle_ec_init_tables, L.oracle_gf_gen_rs_matrix
+        what = "AVX-512+GFNI port of gf_Nvect_dot_prod_avx512_gfni (oracle/ec_gfni_port.c)"
+    else:
+        ref = os.path.join(REPO, "oracle", "_ref", "libisal_ref.so")
+        kind = "reference"
+        if not os.path.exists(ref):
+            ref, kind = os.path.join(REPO, "oracle", "liboracle.so"), "port"
+        if not os.path.exists(ref):
+            return None
+        L = ctypes.CDLL(ref)
+        prefix = "" if kind == "reference" else "oracle_"
+        enc = getattr(L, prefix + "ec_encode_data")
+        init = getattr(L, prefix + "ec_init_tables")
+        gen = getattr(L, prefix + "gf_gen_rs_matrix")
+        what = ("reference ec_base.c (noarch build; no nasm for the AVX-512/GFNI kernels)"
+                if kind == "reference" else "oracle port of ec_base.c")
     u8p = ctypes.POINTER(ctypes.c_ubyte)
     enc.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.POINTER(u8p), ctypes.POINTER(u8p)]
     enc.restype = None
@@ -264,9 +280,8 @@ def cpu_baseline(k, p, n, seconds, threads, check=None):
         "unit": "GiB/s",
         "cores": threads,
         "kind": kind,
-        "sample": f"{stripes} stripes of k={k} p={p} x {n} B, ec_encode_data from "
-                  f"{'reference ec_base.c (noarch; no nasm for the AVX-512/GFNI kernels)' if kind == 'reference' else 'oracle port of ec_base.c'}"
-                  f", {threads} threads x {wall:.1f} s",
+        "sample": f"{stripes} stripes of k={k} p={p} x {n} B, ec_encode_data from {what}, "
+                  f"{threads} threads x {wall:.1f} s",
         "parity_stripe_match": parity_ok,
     }
 
@@ -422,6 +437,10 @@ def main(argv=None):
         if args.workload == "encode":
             check = (data[0].cpu().numpy(), out[0].cpu().numpy())
         result["cpu_baseline"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check)
+        # the reference's fast x86 path cannot be assembled here (no nasm): its
+        # AVX-512+GFNI kernels restated in C intrinsics, timed the same way
+        result["cpu_baseline_simd_port"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check,
+                                                        impl="gfni")
     else:
         result["cpu_baseline"] = None
     if d.rank == 0:

@@ -194,3 +194,28 @@ def test_gf_vect_mul_rejects_bad_length_without_gpu(engine):
         assert engine.gf_vect_mul(n, t, s, d) != 0
         assert engine.gf_vect_mul_base(n, t, s, d) != 0
     assert not d.any()
+
+
+def test_gfni_port_matches_oracle(oracle):
+    """The CPU SIMD baseline (port of the reference's AVX-512+GFNI kernels) is bit-exact."""
+    import ctypes
+    import os
+
+    path = os.path.join(ecutil.ORACLE_DIR, "libgfni_port.so")
+    if not os.path.exists(path):
+        import subprocess
+
+        subprocess.run(["make", "-s", "-C", ecutil.ORACLE_DIR, "libgfni_port.so"], check=True)
+    G = ctypes.CDLL(path)
+    if not G.gfni_port_available():
+        pytest.skip("host CPU lacks AVX-512BW + GFNI")
+    from ecutil import _p, _pp
+
+    for k, rows, n in [(10, 4, 65536), (20, 6, 4096 + 13), (3, 7, 63), (1, 1, 1), (64, 16, 1000), (10, 4, 0)]:
+        coef = fill_bytes(k * rows, k * 100 + rows)
+        t = oracle.ec_init_tables(k, rows, coef)
+        src = [fill_bytes(n, 7 * j + k) for j in range(k)]
+        want = oracle.encode(coef, k, rows, src)
+        got = [np.zeros(n, np.uint8) for _ in range(rows)]
+        G.gfni_port_ec_encode_data(n, k, rows, _p(t), _pp(src), _pp(got))
+        assert all(np.array_equal(a, b) for a, b in zip(got, want)), (k, rows, n)
