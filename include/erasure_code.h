@@ -77,6 +77,63 @@ void gf_vect_mad(int len, int vec, int vec_i, unsigned char *gftbls, unsigned ch
 void gf_vect_mad_base(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src,
                       unsigned char *dest);
 
+/* ---- deprecated per-ISA names (binary compatibility) -------------------- */
+/*
+ * The reference exports x86 per-ISA variants of every data-path function
+ * (erasure_code.h:249-1050, isa-l.def:5-48) for callers built against older
+ * releases. Here each is an alias of the corresponding engine entry point
+ * (same GPU path, same results): gf_Nvect_dot_prod_* == ec_encode_data with
+ * rows = N, gf_Nvect_mad_* == ec_encode_data_update with rows = N. Unlike the
+ * reference SIMD kernels, which return without work for len below their
+ * vector width (e.g. gf_vect_dot_prod_avx512.asm:226-229), these compute for
+ * every len >= 0.
+ */
+#ifndef ISAL_HIP_DEPRECATED
+#define ISAL_HIP_DEPRECATED __attribute__((deprecated))
+#endif
+ISAL_HIP_DEPRECATED void ec_encode_data_sse(int len, int k, int rows, unsigned char *gftbls, unsigned char **data, unsigned char **coding);
+ISAL_HIP_DEPRECATED void ec_encode_data_update_sse(int len, int k, int rows, int vec_i, unsigned char *gftbls, unsigned char *data, unsigned char **coding);
+ISAL_HIP_DEPRECATED void gf_vect_dot_prod_sse(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char *dest);
+ISAL_HIP_DEPRECATED void gf_vect_mad_sse(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char *dest);
+ISAL_HIP_DEPRECATED void gf_2vect_dot_prod_sse(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_2vect_mad_sse(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_3vect_dot_prod_sse(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_3vect_mad_sse(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_4vect_dot_prod_sse(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_4vect_mad_sse(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_5vect_dot_prod_sse(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_5vect_mad_sse(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_6vect_dot_prod_sse(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_6vect_mad_sse(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void ec_encode_data_avx(int len, int k, int rows, unsigned char *gftbls, unsigned char **data, unsigned char **coding);
+ISAL_HIP_DEPRECATED void ec_encode_data_update_avx(int len, int k, int rows, int vec_i, unsigned char *gftbls, unsigned char *data, unsigned char **coding);
+ISAL_HIP_DEPRECATED void gf_vect_dot_prod_avx(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char *dest);
+ISAL_HIP_DEPRECATED void gf_vect_mad_avx(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char *dest);
+ISAL_HIP_DEPRECATED void gf_2vect_dot_prod_avx(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_2vect_mad_avx(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_3vect_dot_prod_avx(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_3vect_mad_avx(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_4vect_dot_prod_avx(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_4vect_mad_avx(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_5vect_dot_prod_avx(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_5vect_mad_avx(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_6vect_dot_prod_avx(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_6vect_mad_avx(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void ec_encode_data_avx2(int len, int k, int rows, unsigned char *gftbls, unsigned char **data, unsigned char **coding);
+ISAL_HIP_DEPRECATED void ec_encode_data_update_avx2(int len, int k, int rows, int vec_i, unsigned char *gftbls, unsigned char *data, unsigned char **coding);
+ISAL_HIP_DEPRECATED void gf_vect_dot_prod_avx2(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char *dest);
+ISAL_HIP_DEPRECATED void gf_vect_mad_avx2(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char *dest);
+ISAL_HIP_DEPRECATED void gf_2vect_dot_prod_avx2(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_2vect_mad_avx2(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_3vect_dot_prod_avx2(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_3vect_mad_avx2(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_4vect_dot_prod_avx2(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_4vect_mad_avx2(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_5vect_dot_prod_avx2(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_5vect_mad_avx2(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_6vect_dot_prod_avx2(int len, int vlen, unsigned char *gftbls, unsigned char **src, unsigned char **dest);
+ISAL_HIP_DEPRECATED void gf_6vect_mad_avx2(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src, unsigned char **dest);
+
 /* ---- GF(2^8) helpers and matrices (host) -------------------------------- */
 
 /* Replaces gf_mul (reference erasure_code.h:1064-1065, ec_base.c:50-63). */

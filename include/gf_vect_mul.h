@@ -33,6 +33,14 @@ void gf_vect_mul_init_base(unsigned char c, unsigned char *gftbl);
  */
 int gf_vect_mul(int len, unsigned char *gftbl, void *src, void *dest);
 
+/* Deprecated per-ISA names (reference gf_vect_mul.h:46-97, isa-l.def:11-12):
+ * aliases of gf_vect_mul. */
+#ifndef ISAL_HIP_DEPRECATED
+#define ISAL_HIP_DEPRECATED __attribute__((deprecated))
+#endif
+ISAL_HIP_DEPRECATED int gf_vect_mul_sse(int len, unsigned char *gftbl, void *src, void *dest);
+ISAL_HIP_DEPRECATED int gf_vect_mul_avx(int len, unsigned char *gftbl, void *src, void *dest);
+
 /* Replaces gf_vect_mul_base (reference gf_vect_mul.h:170-171, ec_base.c:344-358). */
 int gf_vect_mul_base(int len, unsigned char *gftbl, unsigned char *src, unsigned char *dest);
 

@@ -372,3 +372,65 @@ def test_pipe_host_stripes_vs_oracle(engine, oracle, gpu, mode, pinned):
         want = oracle.encode(a[k * k:], k, p, [src[s, j].numpy() for j in range(k)])
         for l in range(p):
             assert np.array_equal(par[s, l].numpy(), want[l]), (mode, pinned, s, l)
+
+
+# --------------------------------------------------------------------------
+# deprecated per-ISA aliases (reference erasure_code.h:249-1050)
+# --------------------------------------------------------------------------
+
+def test_deprecated_per_isa_aliases(engine, oracle, gpu):
+    import ctypes
+
+    L = engine.lib()
+    u8p = ctypes.POINTER(ctypes.c_ubyte)
+
+    def pp(arrs):
+        a = (u8p * len(arrs))()
+        for i, x in enumerate(arrs):
+            a[i] = x.ctypes.data_as(u8p)
+        return a
+
+    n, k = 1000 + 3, 7
+    src = [fill_bytes(n, 40 + j) for j in range(k)]
+    for isa in ("sse", "avx", "avx2"):
+        for N in range(1, 7):
+            coef = fill_bytes(k * N, 10 * N + len(isa))
+            t = oracle.ec_init_tables(k, N, coef)
+            want = oracle.encode(coef, k, N, src)
+            got = [np.zeros(n, np.uint8) for _ in range(N)]
+            if N == 1:
+                getattr(L, f"gf_vect_dot_prod_{isa}")(n, k, t.ctypes.data_as(u8p), pp(src),
+                                                     got[0].ctypes.data_as(u8p))
+            else:
+                getattr(L, f"gf_{N}vect_dot_prod_{isa}")(n, k, t.ctypes.data_as(u8p), pp(src), pp(got))
+            assert all(np.array_equal(a, b) for a, b in zip(got, want)), (isa, N, "dot")
+            # mad: accumulate every source -> the same parity
+            acc = [np.zeros(n, np.uint8) for _ in range(N)]
+            for v in range(k):
+                if N == 1:
+                    getattr(L, f"gf_vect_mad_{isa}")(n, k, v, t.ctypes.data_as(u8p),
+                                                    src[v].ctypes.data_as(u8p), acc[0].ctypes.data_as(u8p))
+                else:
+                    getattr(L, f"gf_{N}vect_mad_{isa}")(n, k, v, t.ctypes.data_as(u8p),
+                                                       src[v].ctypes.data_as(u8p), pp(acc))
+            assert all(np.array_equal(a, b) for a, b in zip(acc, want)), (isa, N, "mad")
+        coef = fill_bytes(k * 4, 99)
+        t = oracle.ec_init_tables(k, 4, coef)
+        got = [np.zeros(n, np.uint8) for _ in range(4)]
+        getattr(L, f"ec_encode_data_{isa}")(n, k, 4, t.ctypes.data_as(u8p), pp(src), pp(got))
+        assert all(np.array_equal(a, b) for a, b in zip(got, oracle.encode(coef, k, 4, src)))
+        upd = [np.zeros(n, np.uint8) for _ in range(4)]
+        for v in range(k):
+            getattr(L, f"ec_encode_data_update_{isa}")(n, k, 4, v, t.ctypes.data_as(u8p),
+                                                       src[v].ctypes.data_as(u8p), pp(upd))
+        assert all(np.array_equal(a, b) for a, b in zip(upd, got))
+    for isa in ("sse", "avx"):
+        f = getattr(L, f"gf_vect_mul_{isa}")
+        f.restype = ctypes.c_int
+        d = np.zeros(96, np.uint8)
+        s = fill_bytes(96, 5)
+        assert f(96, oracle.gf_vect_mul_init(0x53).ctypes.data_as(u8p), ctypes.c_void_p(s.ctypes.data),
+                 ctypes.c_void_p(d.ctypes.data)) == 0
+        assert bytes(d) == bytes(oracle.gf_mul(0x53, int(x)) for x in s)
+        assert f(95, oracle.gf_vect_mul_init(0x53).ctypes.data_as(u8p), ctypes.c_void_p(s.ctypes.data),
+                 ctypes.c_void_p(d.ctypes.data)) != 0
