@@ -173,11 +173,19 @@ __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* _
   }
 }
 
-// Per-byte dot product for columns [off, off+nb) of one stripe (tails, unaligned).
-template <int P>
+// First-mismatch record of the verify kernels: key = column << 8 | row, kept
+// as the minimum over the launch (smallest column, then smallest row there).
+__device__ __forceinline__ void note_mismatch(unsigned long long* bad, long long col, int row) {
+  atomicMin(bad, (static_cast<unsigned long long>(col) << 8) | static_cast<unsigned>(row));
+}
+
+// Per-byte dot product for columns [off, off+nb) of one stripe (tails,
+// unaligned shards). VERIFY: compare with the bytes at dst instead of storing.
+template <int P, bool VERIFY = false>
 __device__ __forceinline__ void dot_bytes(const uint64_t* __restrict__ sp, int src0, int dst0,
                                           const uint32_t* __restrict__ tbl, int k, long long off,
-                                          int nb) {
+                                          int nb, unsigned long long* bad = nullptr, int row0 = 0,
+                                          long long col0 = 0) {
   for (int b = 0; b < nb; ++b) {
     uint32_t acc[P];
 #pragma unroll
@@ -189,8 +197,14 @@ __device__ __forceinline__ void dot_bytes(const uint64_t* __restrict__ sp, int s
       for (int l = 0; l < P; ++l) acc[l] ^= gf_mul4(load_coef(tbl + (j * P + l) * kTbl), s);
     }
 #pragma unroll
-    for (int l = 0; l < P; ++l)
-      reinterpret_cast<uint8_t*>(sp[dst0 + l])[off + b] = static_cast<uint8_t>(acc[l]);
+    for (int l = 0; l < P; ++l) {
+      uint8_t* d = reinterpret_cast<uint8_t*>(sp[dst0 + l]) + off + b;
+      if constexpr (VERIFY) {
+        if (static_cast<uint8_t>(acc[l]) != *d) note_mismatch(bad, col0 + off + b, row0 + l);
+      } else {
+        *d = static_cast<uint8_t>(acc[l]);
+      }
+    }
   }
 }
 
@@ -206,6 +220,25 @@ constexpr int enc_waves() {
   constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8;
   constexpr int w = 512 / est;
   return w > 8 ? 8 : (w < 4 ? 4 : w);
+}
+
+// acc[l] = XOR_j c[l][j] * src[j][off..off+16) for one lane.
+template <int P, class Pol>
+__device__ __forceinline__ void accum16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
+                                        const uint32_t* __restrict__ tbl, int k, long long off) {
+#pragma unroll
+  for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
+  int j = 0;
+  for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::NT_LD>(acc, src, j, off, tbl);
+  // Remainder. The launcher only picks U > 4 when U divides k, so there the
+  // (cheap, correct for any k) single-source loop is dead in practice.
+  if constexpr (Pol::U == 4) {
+    if (j + 2 <= k) {
+      chunk16<P, 2, Pol::NT_LD>(acc, src, j, off, tbl);
+      j += 2;
+    }
+  }
+  for (; j < k; ++j) chunk16<P, 1, Pol::NT_LD>(acc, src, j, off, tbl);
 }
 
 template <int P, class Pol = EncDefault>
@@ -233,20 +266,7 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U>())) void ec_encode_v1
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
       uint32_t acc[P][4];
-#pragma unroll
-      for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
-      const uint64_t* __restrict__ src = sp + src0;
-      int j = 0;
-      for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::NT_LD>(acc, src, j, off, tbl);
-      // Remainder. The launcher only picks U > 4 when U divides k, so there the
-      // (cheap, correct for any k) single-source loop is dead in practice.
-      if constexpr (Pol::U == 4) {
-        if (j + 2 <= k) {
-          chunk16<P, 2, Pol::NT_LD>(acc, src, j, off, tbl);
-          j += 2;
-        }
-      }
-      for (; j < k; ++j) chunk16<P, 1, Pol::NT_LD>(acc, src, j, off, tbl);
+      accum16<P, Pol>(acc, sp + src0, tbl, k, off);
 #pragma unroll
       for (int l = 0; l < P; ++l)
         store16<Pol::NT_ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]));
@@ -268,6 +288,57 @@ __global__ __launch_bounds__(kBlock) void ec_encode_b1(const uint64_t* __restric
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kBlock + threadIdx.x;
     if (off < len) dot_bytes<P>(sp, src0, dst0, tbl, k, off, 1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Verify (xor_check / pq_check): recompute the parity of each column and
+// compare it with the stored rows at dst; the first mismatching (column, row)
+// is reduced into *bad with atomicMin. Nothing is written to the shards.
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(kBlock, (enc_waves<P, 4>())) void ec_verify_v16(
+    const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
+    const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles,
+    unsigned long long* __restrict__ bad, int row0, long long col0) {
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned stripe = w / tiles;
+    const unsigned tile = w - stripe * tiles;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
+    const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
+    if (off + kVec <= len) {
+      uint32_t acc[P][4];
+      accum16<P, EncNT<4>>(acc, sp + src0, tbl, k, off);
+#pragma unroll
+      for (int l = 0; l < P; ++l) {
+        const uint4 e = load16<true>(sp[dst0 + l], off);
+        const uint32_t x[4] = {acc[l][0] ^ e.x, acc[l][1] ^ e.y, acc[l][2] ^ e.z, acc[l][3] ^ e.w};
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          if (x[d]) {
+            note_mismatch(bad, col0 + off + 4 * d + (__builtin_ctz(x[d]) >> 3), row0 + l);
+            break;
+          }
+      }
+    } else if (off < len) {
+      dot_bytes<P, true>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off), bad, row0, col0);
+    }
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(kBlock) void ec_verify_b1(const uint64_t* __restrict__ ptrs,
+                                                       int ptr_stride, int src0, int dst0,
+                                                       const uint32_t* __restrict__ tbl, int len,
+                                                       int k, unsigned nitems, unsigned tiles,
+                                                       unsigned long long* __restrict__ bad,
+                                                       int row0, long long col0) {
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned stripe = w / tiles;
+    const unsigned tile = w - stripe * tiles;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
+    const long long off = static_cast<long long>(tile) * kBlock + threadIdx.x;
+    if (off < len) dot_bytes<P, true>(sp, src0, dst0, tbl, k, off, 1, bad, row0, col0);
   }
 }
 
@@ -441,6 +512,39 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
       }
       if (e != hipSuccess) return static_cast<int>(e);
     }
+  }
+  return 0;
+}
+
+extern "C" int isal_hip_launch_verify(const uint64_t* d_ptrs, int ptr_stride, int src_idx0,
+                                      int dst_idx0, const uint32_t* d_tbl, int len, int k, int rows,
+                                      long long col0, unsigned long long* d_bad, int vec16,
+                                      void* stream) {
+  if (len <= 0 || rows <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned span = vec16 ? kTile : kBlock;
+  const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
+  for (int r0 = 0; r0 < rows; r0 += EC_MAX_ROWS_PER_PASS) {
+    const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
+    const uint32_t* tbl = d_tbl + static_cast<size_t>(kTbl) * k * r0;
+    const int dst0 = dst_idx0 + r0;
+    const unsigned grid = grid_for(tiles);
+    switch (P) {
+#define EC_CASE(n)                                                                            \
+  case n:                                                                                     \
+    if (vec16)                                                                                \
+      hipLaunchKernelGGL(ec_verify_v16<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride, \
+                         src_idx0, dst0, tbl, len, k, tiles, tiles, d_bad, r0, col0);         \
+    else                                                                                      \
+      hipLaunchKernelGGL(ec_verify_b1<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride,  \
+                         src_idx0, dst0, tbl, len, k, tiles, tiles, d_bad, r0, col0);         \
+    break;
+      EC_CASE(1) EC_CASE(2) EC_CASE(3) EC_CASE(4) EC_CASE(5) EC_CASE(6) EC_CASE(7) EC_CASE(8)
+#undef EC_CASE
+    }
+    isal_hip_count_launch();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
   }
   return 0;
 }

@@ -47,6 +47,25 @@ int isal_hip_launch_update(const uint64_t *d_ptrs, int ptr_stride, int src_idx, 
                            const uint32_t *d_tbl, int len, int k, int rows, int vec_i,
                            long long nstripes, int vec16, void *stream);
 
+/* Verify one stripe (nstripes = 1): recompute rows outputs from the sources and
+ * compare with the bytes at the output pointers; *d_bad (preset to ~0 by the
+ * caller) receives min((col0 + column) << 8 | row) over mismatches. */
+int isal_hip_launch_verify(const uint64_t *d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
+                           const uint32_t *d_tbl, int len, int k, int rows, long long col0,
+                           unsigned long long *d_bad, int vec16, void *stream);
+
+/* The shim's generic synchronous call (host or device shard pointers).
+ * op: ISAL_HIP_OP_ENCODE (dst = coded sources, nsrc = k), ISAL_HIP_OP_UPDATE
+ * (dst ^= c[.][vec_i] * src[0], nsrc = 1), ISAL_HIP_OP_VERIFY (compare dst
+ * with the coded sources). Returns ~0, or for VERIFY the first mismatch as
+ * column << 8 | row. */
+#define ISAL_HIP_OP_ENCODE 0
+#define ISAL_HIP_OP_UPDATE 1
+#define ISAL_HIP_OP_VERIFY 2
+unsigned long long isal_hip_run(int op, int len, int k, int rows, int vec_i,
+                                const unsigned char *gftbls, unsigned char *const *src, int nsrc,
+                                unsigned char *const *dst);
+
 /* Launch counter shared by the shim and the launchers. */
 void isal_hip_count_launch(void);
 

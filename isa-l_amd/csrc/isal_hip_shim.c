@@ -211,16 +211,20 @@ on_device(const void *p)
 
 /* ---- the generic synchronous call --------------------------------------- */
 
-enum { OP_ENCODE = 0, OP_UPDATE = 1 };
+enum { OP_ENCODE = ISAL_HIP_OP_ENCODE, OP_UPDATE = ISAL_HIP_OP_UPDATE, OP_VERIFY = ISAL_HIP_OP_VERIFY };
 
 /*
  * OP_ENCODE: dst[l] = XOR_j c[l][j] * src[j], nsrc = k.
  * OP_UPDATE: dst[l] ^= c[l][vec_i] * src[0], nsrc = 1.
+ * OP_VERIFY: compare dst[l] with XOR_j c[l][j] * src[j]; nothing is written.
+ * Returns ~0 (no mismatch / not a verify) or the first mismatch as
+ * column << 8 | row.
  */
-static void
+static unsigned long long
 run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
        unsigned char *const *src, int nsrc, unsigned char *const *dst)
 {
+        unsigned long long first_bad = ~0ull;
         ctx_t *c;
         int nptr = nsrc + rows, i, nstage = 0;
         int dev_flag[512];
@@ -231,13 +235,13 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         long long c0;
 
         if (len <= 0 || rows <= 0 || k < 0)
-                return;
+                return first_bad;
         if (op == OP_UPDATE && (vec_i < 0 || vec_i >= k)) {
                 /* Out-of-range vec_i is undefined in the reference (it reads past
                  * gftbls); here it must not become an out-of-bounds GPU access. */
                 fprintf(stderr, "isal_hip: ec update with vec_i=%d outside [0,%d): ignored\n",
                         vec_i, k);
-                return;
+                return first_bad;
         }
         flag = nptr <= 512 ? dev_flag : (int *) malloc(sizeof(int) * (size_t) nptr);
         if (!flag) {
@@ -268,8 +272,8 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
 
         tbl_dwords = isal_hip_tables_dwords(k, rows);
         ptr_bytes = ((size_t) nptr * 8 + 15) & ~(size_t) 15;
-        args_bytes = ptr_bytes + tbl_dwords * 4;
-        ensure_args(c, args_bytes);
+        args_bytes = ptr_bytes + ((tbl_dwords * 4 + 15) & ~(size_t) 15);
+        ensure_args(c, args_bytes + 16); /* + the verify result word */
         h_ptrs = (uint64_t *) c->h_args;
         h_tbl = (uint32_t *) ((char *) c->h_args + ptr_bytes);
         isal_hip_build_tables(k, rows, gftbls, h_tbl);
@@ -285,8 +289,9 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                         } else {
                                 unsigned char *st = c->d_stage + (size_t) s++ * slot;
                                 d = (uint64_t) (uintptr_t) st;
-                                /* sources, and outputs of a read-modify-write update, go in */
-                                if (i < nsrc || op == OP_UPDATE)
+                                /* sources, and outputs of a read-modify-write update or
+                                 * of a verify, go in */
+                                if (i < nsrc || op != OP_ENCODE)
                                         HIP_OR_DIE(hipMemcpyAsync(st, host + c0, (size_t) clen,
                                                                   hipMemcpyHostToDevice, c->stream));
                         }
@@ -296,6 +301,22 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 }
                 HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, args_bytes, hipMemcpyHostToDevice,
                                           c->stream));
+                if (op == OP_VERIFY) {
+                        unsigned long long *d_bad = (unsigned long long *) ((char *) c->d_args + args_bytes);
+                        HIP_OR_DIE(hipMemsetAsync(d_bad, 0xff, 8, c->stream));
+                        err = isal_hip_launch_verify((const uint64_t *) c->d_args, nptr, 0, nsrc,
+                                                     (const uint32_t *) ((char *) c->d_args + ptr_bytes),
+                                                     clen, k, rows, c0, d_bad, vec16, c->stream);
+                        if (err)
+                                die("kernel launch", (hipError_t) err);
+                        HIP_OR_DIE(hipMemcpyAsync((char *) c->h_args + args_bytes, d_bad, 8,
+                                                  hipMemcpyDeviceToHost, c->stream));
+                        HIP_OR_DIE(hipStreamSynchronize(c->stream));
+                        memcpy(&first_bad, (char *) c->h_args + args_bytes, 8);
+                        if (first_bad != ~0ull)
+                                break;
+                        continue;
+                }
                 if (op == OP_ENCODE)
                         err = isal_hip_launch_encode((const uint64_t *) c->d_args, nptr, 0, nsrc,
                                                      (const uint32_t *) ((char *) c->d_args + ptr_bytes),
@@ -321,6 +342,14 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         }
         if (flag != dev_flag)
                 free(flag);
+        return first_bad;
+}
+
+unsigned long long
+isal_hip_run(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+             unsigned char *const *src, int nsrc, unsigned char *const *dst)
+{
+        return run_ec(op, len, k, rows, vec_i, gftbls, src, nsrc, dst);
 }
 
 /* ---- reference data-path ABI ------------------------------------------- */

@@ -7,7 +7,7 @@
  * cpu_baseline leg may load it, and never as the thing measured or shipped.
  * The product library (isa-l_amd/, libisal_hip.so) does not link it.
  *
- * Parity is pinned: tests/test_oracle_golden.py checks every function here
+ * Parity is pinned: tests/test_golden_cpu.py checks every function here
  * against tests/golden/, which oracle/gen_golden.c produced by linking the
  * reference's own ec_base.c (recipe: oracle/Makefile, target `golden`).
  *
@@ -262,4 +262,86 @@ oracle_fnv1a32(const unsigned char *buf, long long n)
                 h *= 0x01000193u;
         }
         return h;
+}
+
+/* ---- RAID (reference raid/raid_base.c) ----------------------------------- */
+
+/* raid_base.c:100-118 — last vector = XOR of the others; 1 if vects < 3. */
+int
+oracle_xor_gen(int vects, int len, unsigned char **a)
+{
+        int i, j;
+        if (vects < 3)
+                return 1;
+        for (i = 0; i < len; i++) {
+                unsigned char x = a[0][i];
+                for (j = 1; j < vects - 1; j++)
+                        x ^= a[j][i];
+                a[vects - 1][i] = x;
+        }
+        return 0;
+}
+
+/* raid_base.c:120-140 — 0 if all vectors XOR to zero, else 1. */
+int
+oracle_xor_check(int vects, int len, unsigned char **a)
+{
+        int i, j;
+        if (vects < 2)
+                return 1;
+        for (i = 0; i < len; i++) {
+                unsigned char x = 0;
+                for (j = 0; j < vects; j++)
+                        x ^= a[j][i];
+                if (x)
+                        return 1;
+        }
+        return 0;
+}
+
+static unsigned char
+oracle_mul2(unsigned char q)
+{
+        return (unsigned char) ((q << 1) ^ ((q & 0x80) ? 0x1d : 0));
+}
+
+/* raid_base.c:44-68 — P and Q (Horner from the last source: q = D_j ^ 2q);
+ * the reference works on 8-byte words, so only len & ~7 bytes are produced. */
+int
+oracle_pq_gen(int vects, int len, unsigned char **a)
+{
+        int i, j, n = len & ~7;
+        if (vects < 4)
+                return 1;
+        for (i = 0; i < n; i++) {
+                unsigned char p = a[vects - 3][i], q = p;
+                for (j = vects - 4; j >= 0; j--) {
+                        p ^= a[j][i];
+                        q = (unsigned char) (a[j][i] ^ oracle_mul2(q));
+                }
+                a[vects - 2][i] = p;
+                a[vects - 1][i] = q;
+        }
+        return 0;
+}
+
+/* raid_base.c:71-98 — 0, or i|1 (P wrong at byte i) / i|2 (Q wrong). */
+int
+oracle_pq_check(int vects, int len, unsigned char **a)
+{
+        int i, j;
+        if (vects < 4)
+                return 1;
+        for (i = 0; i < len; i++) {
+                unsigned char p = a[vects - 3][i], q = p;
+                for (j = vects - 4; j >= 0; j--) {
+                        p ^= a[j][i];
+                        q = (unsigned char) (a[j][i] ^ oracle_mul2(q));
+                }
+                if (a[vects - 2][i] != p)
+                        return i | 1;
+                if (a[vects - 1][i] != q)
+                        return i | 2;
+        }
+        return 0;
 }

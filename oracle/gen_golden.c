@@ -31,6 +31,11 @@ unsigned char gf_inv(unsigned char a);
 void gf_gen_rs_matrix(unsigned char *a, int m, int k);
 void gf_gen_cauchy1_matrix(unsigned char *a, int m, int k);
 int gf_invert_matrix(unsigned char *in, unsigned char *out, const int n);
+/* Reference raid ABI (reference include/raid.h; raid_base.c via raid_base_aliases.c). */
+int xor_gen(int vects, int len, void **array);
+int xor_check(int vects, int len, void **array);
+int pq_gen(int vects, int len, void **array);
+int pq_check(int vects, int len, void **array);
 
 static FILE *out;
 static int first_item;
@@ -472,6 +477,58 @@ main(int argc, char **argv)
                 put_hex(d, len);
                 fprintf(out, "}");
                 free(s), free(d);
+        }
+        fprintf(out, "]");
+
+        /* RAID (reference raid_base.c): xor_gen / pq_gen outputs, and the
+         * check functions' return values on clean and corrupted arrays. */
+        fprintf(out, ",\n  \"raid\": [");
+        first_item = 1;
+        {
+                static const int lens[] = { 0, 1, 13, 31, 32, 101, 1024, 4096 + 7 };
+                int v, li;
+                for (v = 3; v <= 20; v += (v < 6 ? 1 : 5)) {
+                        for (li = 0; li < (int) (sizeof(lens) / sizeof(lens[0])); li++) {
+                                int len = lens[li], jj, rx, rp, cx, cp, cx2 = -1, cp2 = -1;
+                                unsigned long long seed = 900 + v * 31 + li;
+                                unsigned char *bx[24], *bp[24];
+                                for (jj = 0; jj < v; jj++) {
+                                        bx[jj] = malloc((size_t) len + 1);
+                                        bp[jj] = malloc((size_t) len + 1);
+                                        fill_bytes(bx[jj], len, seed + jj);
+                                        fill_bytes(bp[jj], len, seed + jj);
+                                }
+                                rx = xor_gen(v, len, (void **) bx);
+                                rp = pq_gen(v, len, (void **) bp);
+                                cx = xor_check(v, len, (void **) bx);
+                                cp = pq_check(v, len & ~7, (void **) bp);
+                                if (len >= 8) {
+                                        /* corrupt one byte of a source, check, restore */
+                                        int at = (len & ~7) - 2 - (li % 3), vi = (li + v) % (v > 3 ? v - 2 : 1);
+                                        bx[vi][at] ^= 0x20;
+                                        cx2 = xor_check(v, len, (void **) bx);
+                                        bx[vi][at] ^= 0x20;
+                                        if (v >= 4) {
+                                                bp[vi][at] ^= 0x20;
+                                                cp2 = pq_check(v, len & ~7, (void **) bp);
+                                                bp[vi][at] ^= 0x20;
+                                        }
+                                }
+                                item_sep();
+                                fprintf(out,
+                                        "{\"vects\": %d, \"len\": %d, \"seed\": %llu, \"xor_ret\": %d, "
+                                        "\"pq_ret\": %d, \"xor_check\": %d, \"pq_check\": %d, "
+                                        "\"xor_check_corrupt\": %d, \"pq_check_corrupt\": %d, "
+                                        "\"xor_fnv\": %u, \"p_fnv\": %u, \"q_fnv\": %u}",
+                                        v, len, seed, rx, rp, cx, cp, cx2, cp2,
+                                        fnv1a32(bx[v - 1], len), v >= 4 ? fnv1a32(bp[v - 2], len) : 0,
+                                        v >= 4 ? fnv1a32(bp[v - 1], len) : 0);
+                                for (jj = 0; jj < v; jj++) {
+                                        free(bx[jj]);
+                                        free(bp[jj]);
+                                }
+                        }
+                }
         }
         fprintf(out, "]\n}\n");
         fclose(out);

@@ -136,6 +136,12 @@ class Oracle:
     def gf_vect_mul(self, length, tbl, src, dest):
         return int(self.L.oracle_gf_vect_mul(length, _p(tbl), _p(src), _p(dest)))
 
+    def raid(self, name, vects, length, arrs):
+        """oracle_{xor_gen,xor_check,pq_gen,pq_check} over numpy vectors (in place)."""
+        f = getattr(self.L, "oracle_" + name)
+        f.restype = ctypes.c_int
+        return int(f(vects, length, _pp(arrs)))
+
     def fnv(self, a: np.ndarray) -> int:
         return int(self.L.oracle_fnv1a32(ctypes.c_void_p(a.ctypes.data), a.size))
 

@@ -219,3 +219,22 @@ def test_gfni_port_matches_oracle(oracle):
         got = [np.zeros(n, np.uint8) for _ in range(rows)]
         G.gfni_port_ec_encode_data(n, k, rows, _p(t), _pp(src), _pp(got))
         assert all(np.array_equal(a, b) for a, b in zip(got, want)), (k, rows, n)
+
+
+def _raid_case_arrays(case):
+    v, n = case["vects"], case["len"]
+    return [fill_bytes(n, case["seed"] + j) for j in range(v)]
+
+
+def test_oracle_raid(oracle):
+    """oracle restatement of raid_base.c == the reference's raid_base.c outputs."""
+    for case in golden()["raid"]:
+        v, n = case["vects"], case["len"]
+        bx, bp = _raid_case_arrays(case), _raid_case_arrays(case)
+        assert oracle.raid("xor_gen", v, n, bx) == case["xor_ret"]
+        assert oracle.raid("pq_gen", v, n, bp) == case["pq_ret"]
+        assert oracle.raid("xor_check", v, n, bx) == case["xor_check"]
+        assert oracle.raid("pq_check", v, n & ~7, bp) == case["pq_check"]
+        assert oracle.fnv(bx[v - 1]) == case["xor_fnv"]
+        if v >= 4:
+            assert oracle.fnv(bp[v - 2]) == case["p_fnv"] and oracle.fnv(bp[v - 1]) == case["q_fnv"]

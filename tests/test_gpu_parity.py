@@ -334,7 +334,8 @@ def test_config_c4_streaming_update_k20_p6(engine, oracle, gpu):
 
 CONFORMANCE = ["gf_inverse_test", "gf_vect_mul_test", "gf_vect_mul_base_test",
                "gf_vect_dot_prod_base_test", "gf_vect_dot_prod_test", "gf_vect_mad_test",
-               "erasure_code_base_test", "erasure_code_test", "erasure_code_update_test"]
+               "erasure_code_base_test", "erasure_code_test", "erasure_code_update_test",
+               "xor_gen_test", "pq_gen_test", "xor_check_test", "pq_check_test"]
 
 
 @pytest.mark.parametrize("name", CONFORMANCE)
@@ -434,3 +435,106 @@ def test_deprecated_per_isa_aliases(engine, oracle, gpu):
         assert bytes(d) == bytes(oracle.gf_mul(0x53, int(x)) for x in s)
         assert f(95, oracle.gf_vect_mul_init(0x53).ctypes.data_as(u8p), ctypes.c_void_p(s.ctypes.data),
                  ctypes.c_void_p(d.ctypes.data)) != 0
+
+
+
+# --------------------------------------------------------------------------
+# RAID P+Q (include/raid.h) on the erasure-code kernels
+# --------------------------------------------------------------------------
+
+def _raid_fn(engine, name):
+    import ctypes
+
+    f = getattr(engine.lib(), name)
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    return f
+
+
+def _vp(bufs):
+    import ctypes
+
+    arr = (ctypes.c_void_p * len(bufs))()
+    for i, b in enumerate(bufs):
+        arr[i] = engine_addr(b)
+    return arr
+
+
+def engine_addr(b):
+    import isal_amd
+
+    return isal_amd.addr(b)
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_raid_vs_reference_fixtures(engine, oracle, gpu, where):
+    import torch
+
+    xg, xc = _raid_fn(engine, "xor_gen"), _raid_fn(engine, "xor_check")
+    pg, pgb, pc = _raid_fn(engine, "pq_gen"), _raid_fn(engine, "pq_gen_base"), _raid_fn(engine, "pq_check")
+    for case in golden()["raid"]:
+        v, n = case["vects"], case["len"]
+        mk = lambda: [fill_bytes(n, case["seed"] + j) for j in range(v)]  # noqa: E731
+        bx, bp = mk(), mk()
+        if where == "device":
+            bx = [torch.from_numpy(b).to(gpu) for b in bx]
+            bp = [torch.from_numpy(b).to(gpu) for b in bp]
+        assert xg(v, n, _vp(bx)) == case["xor_ret"], (v, n)
+        assert pgb(v, n, _vp(bp)) == case["pq_ret"], (v, n)  # base semantics: len & ~7 bytes
+        assert xc(v, n, _vp(bx)) == case["xor_check"]
+        assert pc(v, n & ~7, _vp(bp)) == case["pq_check"]
+        hx = [b.cpu().numpy() if where == "device" else b for b in bx]
+        hp = [b.cpu().numpy() if where == "device" else b for b in bp]
+        assert oracle.fnv(hx[v - 1]) == case["xor_fnv"], (v, n)
+        if v >= 4:
+            assert oracle.fnv(hp[v - 2]) == case["p_fnv"] and oracle.fnv(hp[v - 1]) == case["q_fnv"], (v, n)
+        # dispatched pq_gen: the x86 kernels' contract, len % 32 != 0 -> 1, untouched
+        if v >= 4:
+            again = mk()
+            if where == "device":
+                again = [torch.from_numpy(b).to(gpu) for b in again]
+            r = pg(v, n, _vp(again))
+            if n == 0 or n % 32 == 0:
+                assert r == 0
+            else:
+                assert r == 1
+    # corruption results: positions exactly as gen_golden.c chose them
+    for case in golden()["raid"]:
+        v, n = case["vects"], case["len"]
+        if n < 8:
+            continue
+        li = [0, 1, 13, 31, 32, 101, 1024, 4096 + 7].index(n)
+        at, vi = (n & ~7) - 2 - (li % 3), (li + v) % (v - 2 if v > 3 else 1)
+        bx = [fill_bytes(n, case["seed"] + j) for j in range(v)]
+        xg(v, n, _vp(bx))
+        bx[vi][at] ^= 0x20
+        assert xc(v, n, _vp(bx)) == case["xor_check_corrupt"]
+        if v >= 4:
+            bp = [fill_bytes(n, case["seed"] + j) for j in range(v)]
+            pgb(v, n, _vp(bp))
+            bp[vi][at] ^= 0x20
+            assert pc(v, n & ~7, _vp(bp)) == case["pq_check_corrupt"], (v, n, vi, at)
+
+
+def test_raid_pq_large_and_every_corruption_position(engine, oracle, gpu):
+    """pq_check localises corruption like raid_base.c:96-99 at any byte of any vector."""
+    import torch
+
+    pg, pc = _raid_fn(engine, "pq_gen"), _raid_fn(engine, "pq_check")
+    v, n = 12, 1 << 20
+    bufs = [torch.from_numpy(fill_bytes(n, 77 + j)).to(gpu) for j in range(v)]
+    assert pg(v, n, _vp(bufs)) == 0
+    h = [b.cpu().numpy() for b in bufs]
+    ref = [x.copy() for x in h]
+    assert oracle.raid("pq_gen", v, n, ref) == 0
+    assert all(np.array_equal(a, b) for a, b in zip(h, ref))
+    assert pc(v, n, _vp(bufs)) == 0
+    rng = np.random.default_rng(5)
+    for _ in range(12):
+        j, i = int(rng.integers(0, v)), int(rng.integers(0, n))
+        old = int(bufs[j][i])
+        bufs[j][i] = old ^ 0x41
+        want = [x.copy() for x in h]
+        want[j][i] ^= 0x41
+        assert pc(v, n, _vp(bufs)) == oracle.raid("pq_check", v, n, want), (j, i)
+        bufs[j][i] = old
