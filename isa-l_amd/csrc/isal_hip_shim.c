@@ -213,6 +213,101 @@ on_device(const void *p)
 
 enum { OP_ENCODE = ISAL_HIP_OP_ENCODE, OP_UPDATE = ISAL_HIP_OP_UPDATE, OP_VERIFY = ISAL_HIP_OP_VERIFY };
 
+/* Host-staged calls up to this many staged bytes are packed through the pinned
+ * argument buffer (one H2D + one D2H DMA per call instead of one pageable copy
+ * per shard): the reference's own tests make ~10^5 such calls of a few KiB. */
+#define SMALL_STAGE_BYTES ((size_t) 4 << 20)
+
+static void launch_op(ctx_t *c, int op, size_t ptr_bytes, size_t args_bytes, int nptr, int nsrc,
+                      int clen, long long c0, int k, int rows, int vec_i, int vec16);
+
+static unsigned long long
+run_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+          unsigned char *const *src, int nsrc, unsigned char *const *dst, const int *flag,
+          int nstage)
+{
+        int nptr = nsrc + rows, i, s, first_out = -1, vec16 = 1;
+        size_t slot = ((size_t) len + 255) & ~(size_t) 255;
+        size_t tbl_dwords = isal_hip_tables_dwords(k, rows);
+        size_t ptr_bytes = ((size_t) nptr * 8 + 15) & ~(size_t) 15;
+        size_t args_bytes = ptr_bytes + ((tbl_dwords * 4 + 15) & ~(size_t) 15);
+        size_t stage_off = args_bytes + 16, upload = stage_off;
+        unsigned char *hs, *ds;
+        uint64_t *h_ptrs;
+        unsigned long long first_bad = ~0ull;
+
+        ensure_args(c, stage_off + slot * (size_t) nstage);
+        h_ptrs = (uint64_t *) c->h_args;
+        isal_hip_build_tables(k, rows, gftbls, (uint32_t *) ((char *) c->h_args + ptr_bytes));
+        hs = (unsigned char *) c->h_args + stage_off;
+        ds = (unsigned char *) c->d_args + stage_off;
+        for (i = 0, s = 0; i < nptr; i++) {
+                unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
+                uint64_t d;
+                if (flag[i]) {
+                        d = (uint64_t) (uintptr_t) host;
+                } else {
+                        d = (uint64_t) (uintptr_t) (ds + (size_t) s * slot);
+                        if (i < nsrc || op != OP_ENCODE) {
+                                memcpy(hs + (size_t) s * slot, host, (size_t) len);
+                                upload = stage_off + (size_t) (s + 1) * slot;
+                        }
+                        if (i >= nsrc && first_out < 0)
+                                first_out = s;
+                        s++;
+                }
+                h_ptrs[i] = d;
+                if (d & 15)
+                        vec16 = 0;
+        }
+        HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, upload, hipMemcpyHostToDevice, c->stream));
+        launch_op(c, op, ptr_bytes, args_bytes, nptr, nsrc, len, 0, k, rows, vec_i, vec16);
+        if (op != OP_VERIFY && first_out >= 0)
+                HIP_OR_DIE(hipMemcpyAsync(hs + (size_t) first_out * slot, ds + (size_t) first_out * slot,
+                                          (size_t) (nstage - first_out) * slot, hipMemcpyDeviceToHost,
+                                          c->stream));
+        HIP_OR_DIE(hipStreamSynchronize(c->stream));
+        if (op == OP_VERIFY) {
+                memcpy(&first_bad, (char *) c->h_args + args_bytes, 8);
+                return first_bad;
+        }
+        for (i = nsrc, s = first_out; i < nptr && s >= 0; i++)
+                if (!flag[i])
+                        memcpy(dst[i - nsrc], hs + (size_t) s++ * slot, (size_t) len);
+        return first_bad;
+}
+
+/* Enqueue the kernel(s) of one chunk on c->stream; for OP_VERIFY also reset
+ * the device result word (at d_args + args_bytes) and copy it back to the
+ * same offset of the pinned buffer. */
+static void
+launch_op(ctx_t *c, int op, size_t ptr_bytes, size_t args_bytes, int nptr, int nsrc, int clen,
+          long long c0, int k, int rows, int vec_i, int vec16)
+{
+        const uint64_t *d_ptrs = (const uint64_t *) c->d_args;
+        const uint32_t *d_tbl = (const uint32_t *) ((char *) c->d_args + ptr_bytes);
+        int err;
+        if (op == OP_VERIFY) {
+                unsigned long long *d_bad = (unsigned long long *) ((char *) c->d_args + args_bytes);
+                HIP_OR_DIE(hipMemsetAsync(d_bad, 0xff, 8, c->stream));
+                err = isal_hip_launch_verify(d_ptrs, nptr, 0, nsrc, d_tbl, clen, k, rows, c0, d_bad,
+                                             vec16, c->stream);
+                if (err)
+                        die("kernel launch", (hipError_t) err);
+                HIP_OR_DIE(hipMemcpyAsync((char *) c->h_args + args_bytes, d_bad, 8,
+                                          hipMemcpyDeviceToHost, c->stream));
+                return;
+        }
+        if (op == OP_ENCODE)
+                err = isal_hip_launch_encode(d_ptrs, nptr, 0, nsrc, d_tbl, clen, k, rows, 1, vec16,
+                                             c->stream);
+        else
+                err = isal_hip_launch_update(d_ptrs, nptr, 0, nsrc, d_tbl, clen, k, rows, vec_i, 1,
+                                             vec16, c->stream);
+        if (err)
+                die("kernel launch", (hipError_t) err);
+}
+
 /*
  * OP_ENCODE: dst[l] = XOR_j c[l][j] * src[j], nsrc = k.
  * OP_UPDATE: dst[l] ^= c[l][vec_i] * src[0], nsrc = 1.
@@ -256,6 +351,14 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 nstage += !flag[i];
         }
 
+        if (nstage && (size_t) len * (size_t) nstage <= SMALL_STAGE_BYTES) {
+                unsigned long long r = run_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst,
+                                                 flag, nstage);
+                if (flag != dev_flag)
+                        free(flag);
+                return r;
+        }
+
         /* Column chunk: whole shard when nothing is staged. */
         if (nstage) {
                 size_t per = stage_limit() / (size_t) nstage;
@@ -280,7 +383,7 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
 
         for (c0 = 0; c0 < len; c0 += (long long) chunk) {
                 int clen = (int) ((long long) len - c0 < (long long) chunk ? len - c0 : (long long) chunk);
-                int s = 0, vec16 = 1, err;
+                int s = 0, vec16 = 1;
                 for (i = 0; i < nptr; i++) {
                         unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
                         uint64_t d;
@@ -301,32 +404,14 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 }
                 HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, args_bytes, hipMemcpyHostToDevice,
                                           c->stream));
+                launch_op(c, op, ptr_bytes, args_bytes, nptr, nsrc, clen, c0, k, rows, vec_i, vec16);
                 if (op == OP_VERIFY) {
-                        unsigned long long *d_bad = (unsigned long long *) ((char *) c->d_args + args_bytes);
-                        HIP_OR_DIE(hipMemsetAsync(d_bad, 0xff, 8, c->stream));
-                        err = isal_hip_launch_verify((const uint64_t *) c->d_args, nptr, 0, nsrc,
-                                                     (const uint32_t *) ((char *) c->d_args + ptr_bytes),
-                                                     clen, k, rows, c0, d_bad, vec16, c->stream);
-                        if (err)
-                                die("kernel launch", (hipError_t) err);
-                        HIP_OR_DIE(hipMemcpyAsync((char *) c->h_args + args_bytes, d_bad, 8,
-                                                  hipMemcpyDeviceToHost, c->stream));
                         HIP_OR_DIE(hipStreamSynchronize(c->stream));
                         memcpy(&first_bad, (char *) c->h_args + args_bytes, 8);
                         if (first_bad != ~0ull)
                                 break;
                         continue;
                 }
-                if (op == OP_ENCODE)
-                        err = isal_hip_launch_encode((const uint64_t *) c->d_args, nptr, 0, nsrc,
-                                                     (const uint32_t *) ((char *) c->d_args + ptr_bytes),
-                                                     clen, k, rows, 1, vec16, c->stream);
-                else
-                        err = isal_hip_launch_update((const uint64_t *) c->d_args, nptr, 0, nsrc,
-                                                     (const uint32_t *) ((char *) c->d_args + ptr_bytes),
-                                                     clen, k, rows, vec_i, 1, vec16, c->stream);
-                if (err)
-                        die("kernel launch", (hipError_t) err);
                 s = 0; /* staged slots are in pointer order: outputs follow sources */
                 for (i = 0; i < nptr; i++) {
                         if (flag[i])
