@@ -260,6 +260,7 @@ run_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
                 if (d & 15)
                         vec16 = 0;
         }
+        memset((char *) c->h_args + args_bytes, 0xff, 8);
         HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, upload, hipMemcpyHostToDevice, c->stream));
         launch_op(c, op, ptr_bytes, args_bytes, nptr, nsrc, len, 0, k, rows, vec_i, vec16);
         if (op != OP_VERIFY && first_out >= 0)
@@ -277,9 +278,9 @@ run_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
         return first_bad;
 }
 
-/* Enqueue the kernel(s) of one chunk on c->stream; for OP_VERIFY also reset
- * the device result word (at d_args + args_bytes) and copy it back to the
- * same offset of the pinned buffer. */
+/* Enqueue the kernel(s) of one chunk on c->stream; for OP_VERIFY the result
+ * word (at d_args + args_bytes, uploaded as ~0) is copied back to the same
+ * offset of the pinned buffer. */
 static void
 launch_op(ctx_t *c, int op, size_t ptr_bytes, size_t args_bytes, int nptr, int nsrc, int clen,
           long long c0, int k, int rows, int vec_i, int vec16)
@@ -288,8 +289,9 @@ launch_op(ctx_t *c, int op, size_t ptr_bytes, size_t args_bytes, int nptr, int n
         const uint32_t *d_tbl = (const uint32_t *) ((char *) c->d_args + ptr_bytes);
         int err;
         if (op == OP_VERIFY) {
+                /* the result word was preset to ~0 in the pinned buffer and
+                 * arrived with the argument upload */
                 unsigned long long *d_bad = (unsigned long long *) ((char *) c->d_args + args_bytes);
-                HIP_OR_DIE(hipMemsetAsync(d_bad, 0xff, 8, c->stream));
                 err = isal_hip_launch_verify(d_ptrs, nptr, 0, nsrc, d_tbl, clen, k, rows, c0, d_bad,
                                              vec16, c->stream);
                 if (err)
@@ -402,8 +404,9 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                         if (d & 15)
                                 vec16 = 0;
                 }
-                HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, args_bytes, hipMemcpyHostToDevice,
-                                          c->stream));
+                memset((char *) c->h_args + args_bytes, 0xff, 8);
+                HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, args_bytes + 16,
+                                          hipMemcpyHostToDevice, c->stream));
                 launch_op(c, op, ptr_bytes, args_bytes, nptr, nsrc, clen, c0, k, rows, vec_i, vec16);
                 if (op == OP_VERIFY) {
                         HIP_OR_DIE(hipStreamSynchronize(c->stream));

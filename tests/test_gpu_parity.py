@@ -338,14 +338,45 @@ CONFORMANCE = ["gf_inverse_test", "gf_vect_mul_test", "gf_vect_mul_base_test",
                "xor_gen_test", "pq_gen_test", "xor_check_test", "pq_check_test"]
 
 
+# xor_check_test / pq_check_test sweep every (length, error position, vector)
+# with ~1.6e7 synchronous calls each; at a ~25-30 us GPU round trip per call
+# that is ~8-10 minutes apiece, so they run only with ISAL_SLOW_CONFORMANCE=1
+# (their logs: profiles/r01_slow_conformance.log).
+SLOW_CONFORMANCE = {"xor_check_test", "pq_check_test"}
+
+
+def _run_streaming(exe, timeout):
+    """Run a test program, echoing a heartbeat so long runs visibly progress."""
+    import time
+
+    p = subprocess.Popen([exe], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    t0 = time.time()
+    out = []
+    while True:
+        try:
+            o, _ = p.communicate(timeout=60)
+            out.append(o)
+            break
+        except subprocess.TimeoutExpired:
+            print(f"[{os.path.basename(exe)}: running {time.time() - t0:.0f} s]", flush=True)
+            if time.time() - t0 > timeout:
+                p.kill()
+                o, _ = p.communicate()
+                out.append(o)
+                break
+    return p.returncode, "".join(out)
+
+
 @pytest.mark.parametrize("name", CONFORMANCE)
 def test_reference_test_programs(name, gpu):
+    if name in SLOW_CONFORMANCE and not os.environ.get("ISAL_SLOW_CONFORMANCE"):
+        pytest.skip("~1.6e7 synchronous calls; set ISAL_SLOW_CONFORMANCE=1")
     exe = os.path.join(ecutil.REF_DIR, "conformance", name)
     if not os.path.exists(exe):
         pytest.skip(f"{name} not built (make -C oracle conformance needs /root/reference)")
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=900)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    assert "Pass" in r.stdout or "pass" in r.stdout.lower()
+    rc, out = _run_streaming(exe, timeout=1500)
+    assert rc == 0, out[-3000:]
+    assert "Pass" in out or "pass" in out.lower()
 
 
 # --------------------------------------------------------------------------
