@@ -57,6 +57,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all cores of this rank (<=16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N>1 control-plane backend (nccl = RCCL over xGMI; gloo lets several "
+                         "ranks share one GPU for testing)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the distributed harness without a GPU (gloo, dummy step)")
     return ap.parse_args(argv)
@@ -67,31 +70,36 @@ def parse_args(argv=None):
 # ---------------------------------------------------------------------------
 
 class Dist:
-    def __init__(self, dry: bool):
+    def __init__(self, dry: bool, backend: str = "nccl"):
         self.rank = int(os.environ.get("RANK", 0))
         self.world = int(os.environ.get("WORLD_SIZE", 1))
         self.local_rank = int(os.environ.get("LOCAL_RANK", 0))
+        self.gpu = self.local_rank
         self.dist = None
         self.backend = None
+        if not dry:
+            import torch
+
+            # one process per GPU; ranks beyond the device count (gloo tests) share
+            self.gpu = self.local_rank % max(1, torch.cuda.device_count())
         if self.world > 1:
             import torch.distributed as dist
 
-            self.backend = "gloo" if dry else "nccl"  # nccl == RCCL on ROCm
-            if dry:
+            self.backend = "gloo" if dry else backend  # nccl == RCCL on ROCm
+            if self.backend == "gloo":
                 dist.init_process_group(self.backend)
             else:
                 import torch
 
                 # bind this rank's GPU first so RCCL builds its communicator on it
-                torch.cuda.set_device(self.local_rank)
-                dist.init_process_group(self.backend,
-                                        device_id=torch.device("cuda", self.local_rank))
+                torch.cuda.set_device(self.gpu)
+                dist.init_process_group(self.backend, device_id=torch.device("cuda", self.gpu))
             self.dist = dist
 
     def _dev(self):
         import torch
 
-        return torch.device("cpu") if self.backend == "gloo" else torch.device("cuda", self.local_rank)
+        return torch.device("cpu") if self.backend == "gloo" else torch.device("cuda", self.gpu)
 
     def barrier(self):
         if self.dist:
@@ -292,7 +300,7 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference"):
 
 def main(argv=None):
     args = parse_args(argv)
-    d = Dist(args.dry_run)
+    d = Dist(args.dry_run, args.dist_backend)
     if args.dry_run:
         return dry_run(args, d)
 
@@ -301,8 +309,8 @@ def main(argv=None):
 
     import isal_amd
 
-    torch.cuda.set_device(d.local_rank)
-    dev = torch.device("cuda", d.local_rank)
+    torch.cuda.set_device(d.gpu)
+    dev = torch.device("cuda", d.gpu)
     k, p, n, S = args.k, args.p, args.len, args.stripes
     a = np.frombuffer(control_plane_matrix(d, k, p), dtype=np.uint8)
     if args.workload.startswith("e2e"):
@@ -385,6 +393,21 @@ def main(argv=None):
     wall = d.max(t1 - t0)
     launch_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
 
+    # Self-check on this rank's own batch (no oracle): Vandermonde parity row 0
+    # is all ones, so it must equal the XOR of the sources; decode must return
+    # exactly the erased shards. Reduced with MIN over ranks.
+    ok = True
+    if args.workload == "encode":
+        for s_ in sorted({0, S // 2, S - 1}):
+            x = data[s_, 0].clone()
+            for j in range(1, k):
+                x ^= data[s_, j]
+            ok &= bool(torch.equal(x, out[s_, 0]))
+    elif args.workload == "decode":
+        for i, e in enumerate(errs):
+            ok &= bool(torch.equal(out[:, i], data[:, e]))
+    self_check = None if args.workload == "update" else bool(d.max(0.0 if ok else 1.0) == 0.0)
+
     if args.workload == "update":
         step_bytes = (1 + 2 * p) * n * S
     elif args.workload == "decode":
@@ -414,6 +437,7 @@ def main(argv=None):
             "parallelism": f"stripes sharded over {d.world} GPU(s), no data-path collective",
         },
         "payload_gib_s": round(k * n * S * args.steps * d.world / wall / GIB, 2),
+        "self_check": self_check,
         "roofline": {
             "bound": "hbm",
             "kernel": kernel,
@@ -478,7 +502,7 @@ def e2e(args, d: Dist, a, k, p, n):
     total = (k + p) * n * args.steps * d.world
     # spot check: the last stripe's parity equals a device-resident re-encode
     r = (i[0] - 1) % ring
-    dsrc = src[r].to(dev := torch.device("cuda", d.local_rank))
+    dsrc = src[r].to(dev := torch.device("cuda", d.gpu))
     dpar = torch.empty((p, n), dtype=torch.uint8, device=dev)
     isal_amd.ec_encode_data(n, k, p, isal_amd.ec_init_tables(k, p, a[k * k:]),
                             [dsrc[j] for j in range(k)], [dpar[l] for l in range(p)])

@@ -569,3 +569,31 @@ def test_raid_pq_large_and_every_corruption_position(engine, oracle, gpu):
         want[j][i] ^= 0x41
         assert pc(v, n, _vp(bufs)) == oracle.raid("pq_check", v, n, want), (j, i)
         bufs[j][i] = old
+
+
+# --------------------------------------------------------------------------
+# the N>1 bench path with real GPU work (two ranks share GPU 0 over gloo;
+# RCCL itself needs one GPU per rank and is exercised by the 8-GPU driver run)
+# --------------------------------------------------------------------------
+
+def test_bench_two_ranks_on_one_gpu(gpu):
+    import json
+    import socket
+    import sys
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ecutil.REPO, "bench.py"), "--dist-backend", "gloo", "--stripes", "64",
+           "--len", "65536", "--steps", "4", "--warmup", "1"]
+    for workload in ("encode", "decode"):
+        r = subprocess.run(cmd + ["--workload", workload], capture_output=True, text=True,
+                           timeout=600, cwd=ecutil.REPO)
+        assert r.returncode == 0, r.stderr[-3000:]
+        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        out = json.loads(lines[0])
+        assert out["n_gpus"] == 2 and out["value"] > 0 and out["self_check"] is True, out
