@@ -61,6 +61,72 @@ __global__ __launch_bounds__(256) void mem_pattern(const uint64_t* __restrict__ 
   }
 }
 
+// Same pattern through buffer_load/store with explicit cache-policy bits
+// (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16).
+template <int R, int W, int AUX_LD, int AUX_ST>
+__global__ __launch_bounds__(256) void mem_pattern_buf(const uint64_t* __restrict__ ptrs, int stride,
+                                                       int len, unsigned nitems, unsigned tiles,
+                                                       uint32_t* __restrict__ sink) {
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned stripe = w / tiles, tile = w - stripe * tiles;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * stride;
+    const int off = static_cast<int>(tile) * kTile + threadIdx.x * kVec;
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    v4i a = {static_cast<int>(w), 1, 2, 3};
+    v4i x[R > 0 ? R : 1];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)sp[j], 0, len, 0x00020000);
+      x[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX_LD);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) a ^= x[j];
+    if constexpr (W == 0) {
+      if ((a.x ^ a.y ^ a.z ^ a.w) == 0x1E3779B9) sink[threadIdx.x] = a.x;
+    }
+#pragma unroll
+    for (int l = 0; l < W; ++l) {
+      auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)sp[10 + l], 0, len, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b128(a, rs, off, 0, AUX_ST);
+      a.x += 1;
+    }
+  }
+}
+
+// Two 4 KiB tiles per work item (each wave streams 2 KiB contiguous per shard).
+template <int R, int W>
+__global__ __launch_bounds__(256) void mem_pattern_2t(const uint64_t* __restrict__ ptrs, int stride,
+                                                      int len, unsigned nitems, unsigned tiles,
+                                                      uint32_t* __restrict__ sink) {
+  const unsigned half = tiles / 2;
+  for (unsigned w = blockIdx.x; w < nitems / 2; w += gridDim.x) {
+    const unsigned stripe = w / half, tp = w - stripe * half;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * stride;
+    // wave-contiguous: wave v covers bytes [tp*8K + v*2K, +2K)
+    const unsigned wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long off0 = static_cast<long long>(tp) * 2 * kTile + wave * 2048 + lane * 16;
+    uint4 a0 = make_uint4(w, 1, 2, 3), a1 = a0;
+    uint4 x0[R], x1[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      x0[j] = load16<true>(sp[j], off0);
+      x1[j] = load16<true>(sp[j], off0 + 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      a0.x ^= x0[j].x; a0.y ^= x0[j].y; a0.z ^= x0[j].z; a0.w ^= x0[j].w;
+      a1.x ^= x1[j].x; a1.y ^= x1[j].y; a1.z ^= x1[j].z; a1.w ^= x1[j].w;
+    }
+#pragma unroll
+    for (int l = 0; l < W; ++l) {
+      store16<true>(sp[10 + l], off0, a0);
+      store16<true>(sp[10 + l], off0 + 1024, a1);
+      a0.x += 1;
+      a1.x += 1;
+    }
+  }
+}
+
 __global__ void copy16(const uint4* __restrict__ s, uint4* __restrict__ d, size_t n16) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16;
        i += (size_t)gridDim.x * blockDim.x)
@@ -165,6 +231,21 @@ int main(int argc, char** argv) {
   PATTERN(10, 4, true, true, "mem read10+write4 nt/nt")
   PATTERN(10, 4, false, true, "mem read10+write4 ld/nt")
   PATTERN(10, 0, false, false, "mem read10 only")
+#define PATTERNB(LD, ST, NAME)                                                                 \
+  V.push_back({NAME, 14.0 * shard * S, [=](hipStream_t st) {                                    \
+                 hipLaunchKernelGGL((mem_pattern_buf<10, 4, LD, ST>), dim3(nitems), dim3(256), 0, \
+                                    st, d_ptrs, stride, len, nitems, tiles, (uint32_t*)sinkp);  \
+               }});
+  PATTERNB(2, 2, "buf r10w4 nt/nt")
+  PATTERNB(0x12, 0x12, "buf r10w4 sc1nt/sc1nt")
+  PATTERNB(0x13, 0x13, "buf r10w4 sc0sc1nt/sc0sc1nt")
+  PATTERNB(0x10, 0x10, "buf r10w4 sc1/sc1")
+  PATTERNB(2, 0x12, "buf r10w4 nt/sc1nt")
+  PATTERNB(3, 3, "buf r10w4 sc0nt/sc0nt")
+  V.push_back({"mem r10w4 nt 2 tiles/item", 14.0 * shard * S, [=](hipStream_t st) {
+                 hipLaunchKernelGGL((mem_pattern_2t<10, 4>), dim3(nitems / 2), dim3(256), 0, st,
+                                    d_ptrs, stride, len, nitems, tiles, (uint32_t*)sinkp);
+               }});
   PATTERN(0, 4, false, false, "mem write4 only")
   // first half of the parity buffer copied onto its second half: cbytes moved
   // (the source shards are never written, so encode outputs stay comparable)
@@ -223,7 +304,12 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(out.data() + cbytes / S, coding + cbytes - cbytes / S, cbytes / S,
                  hipMemcpyDeviceToHost));
   };
-  V[7].run(st);  // encode default
+  // reference parity from the default encode variant
+  for (auto& v : V)
+    if (v.encode) {
+      v.run(st);
+      break;
+    }
   grab(want);
 
   for (int r = 0; r < rounds; ++r) {

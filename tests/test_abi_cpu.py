@@ -74,3 +74,44 @@ def test_library_has_no_oracle_dependency():
     assert "oracle_" not in out
     ldd = subprocess.run(["ldd", ecutil.ENGINE_LIB], capture_output=True, text=True).stdout
     assert "oracle" not in ldd and "isal_ref" not in ldd
+
+
+def test_extension_api_rejects_bad_arguments_without_gpu(engine):
+    """isal_hip.h calls validate before touching the GPU and return ISAL_HIP_EINVAL (-1)."""
+    L = engine.lib()
+    h = ctypes.c_void_p()
+    u8p = ctypes.POINTER(ctypes.c_ubyte)
+    tbl = (ctypes.c_ubyte * 64)()
+    ptrs = (u8p * 4)()
+    ok_args = dict(len_=64, k=2, rows=2, n=1)
+    cases = [(-1, 2, 2, 1), (64, 2, 0, 1), (64, 2, 2, 0), (64, -1, 2, 1)]
+    for len_, k, rows, n in cases:
+        assert L.isal_hip_batch_create(ctypes.byref(h), len_, k, rows, tbl, n, ptrs, ptrs) == -1
+    assert L.isal_hip_batch_create(None, 64, 2, 2, tbl, 1, ptrs, ptrs) == -1
+    assert L.isal_hip_batch_create(ctypes.byref(h), 64, 2, 2, None, 1, ptrs, ptrs) == -1
+    assert L.isal_hip_batch_encode(None, None) == -1
+    assert L.isal_hip_batch_update(None, 0, None) == -1
+    assert L.isal_hip_batch_destroy(None) == 0
+    f = L.isal_hip_pipe_create
+    f.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    assert f(ctypes.byref(h), 64, 2, 2, ctypes.cast(tbl, ctypes.c_void_p), 3, 7) == -1  # bad mode
+    assert f(ctypes.byref(h), 0, 2, 2, ctypes.cast(tbl, ctypes.c_void_p), 3, 0) == -1
+    assert f(ctypes.byref(h), 64, 2, 2, ctypes.cast(tbl, ctypes.c_void_p), 0, 0) == -1
+    assert L.isal_hip_pipe_flush(None) == -1
+    assert L.isal_hip_pipe_destroy(None) == 0
+    del ok_args
+
+
+def test_raid_argument_contracts_without_gpu(engine):
+    """raid.h return codes that need no data pass (reference raid_base.c / pq_gen_avx512.asm)."""
+    L = engine.lib()
+    arr = (ctypes.c_void_p * 4)()
+    for name in ("xor_gen", "xor_gen_base"):
+        assert getattr(L, name)(2, 64, arr) == 1  # vects < 3
+    for name in ("pq_gen", "pq_gen_base", "pq_check", "pq_check_base"):
+        assert getattr(L, name)(3, 64, arr) == 1  # vects < 4
+    for name in ("xor_check", "xor_check_base"):
+        assert getattr(L, name)(1, 64, arr) == 1  # vects < 2
+    assert L.pq_gen(4, 33, arr) == 1  # len % 32 on the dispatched path
+    assert L.pq_gen(4, 0, arr) == 0

@@ -37,5 +37,48 @@ main(void)
         for (r = 0; r < REPS * V; r++)
                 (void) hipPointerGetAttributes(&a, b[r % V]);
         printf("hipPointerGetAttributes(host): %.2f us\n", (now() - t) / (REPS * V) * 1e6);
+        {
+                void *h, *d;
+                hipStream_t st;
+                (void) hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+                (void) hipHostMalloc(&h, 1 << 20, 0);
+                (void) hipMalloc(&d, 1 << 20);
+                t = now();
+                for (r = 0; r < REPS; r++) {
+                        (void) hipMemcpyAsync(d, h, 20 * 1024, hipMemcpyHostToDevice, st);
+                        (void) hipStreamSynchronize(st);
+                }
+                printf("H2D 20 KiB pinned + sync: %.1f us\n", (now() - t) / REPS * 1e6);
+                t = now();
+                for (r = 0; r < REPS; r++) {
+                        (void) hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);
+                        (void) hipStreamSynchronize(st);
+                }
+                printf("D2H 8 B pinned + sync: %.1f us\n", (now() - t) / REPS * 1e6);
+                t = now();
+                for (r = 0; r < REPS; r++) {
+                        (void) hipMemsetAsync(d, 0xff, 8, st);
+                        (void) hipStreamSynchronize(st);
+                }
+                printf("memset 8 B + sync: %.1f us\n", (now() - t) / REPS * 1e6);
+                t = now();
+                for (r = 0; r < REPS; r++) {
+                        (void) hipMemcpyAsync(d, h, 20 * 1024, hipMemcpyHostToDevice, st);
+                        (void) hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);
+                        (void) hipStreamSynchronize(st);
+                }
+                printf("H2D 20 KiB + D2H 8 B + one sync: %.1f us\n", (now() - t) / REPS * 1e6);
+                {
+                        void *dv[V];
+                        for (i = 0; i < V; i++) {
+                                (void) hipMalloc(&dv[i], N);
+                                (void) hipMemcpy(dv[i], b[i], N, hipMemcpyHostToDevice);
+                        }
+                        t = now();
+                        for (r = 0; r < REPS; r++)
+                                xor_check(V, N, dv);
+                        printf("xor_check device 17x1KiB: %.1f us/call\n", (now() - t) / REPS * 1e6);
+                }
+        }
         return 0;
 }
