@@ -66,39 +66,64 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const u32x4 __attribute__((address_space(1)))* gload_t;
 typedef u32x4 __attribute__((address_space(1)))* gstore_t;
 
-template <bool NT = false>
-__device__ __forceinline__ uint4 load16(uint64_t base, long long off) {
+// Memory access modes: 0 plain global, 1 non-temporal global (nt),
+// 2 non-temporal buffer_load/store (wave-uniform descriptor per shard, 32-bit
+// lane offset; measured +1.3 % over mode 1 on the 10-read/4-write stream,
+// profiles/r01_probe_variants_3.txt). `len` bounds the buffer descriptor.
+enum : int { kPlain = 0, kNT = 1, kBufNT = 2 };
+
+template <int MODE = kPlain>
+__device__ __forceinline__ uint4 load16(uint64_t base, long long off, int len = 0) {
   u32x4 v;
-  if constexpr (NT)
+  if constexpr (MODE == kBufNT) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
+    const v4i r = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(off), 0, 2 /* nt */);
+    v = {static_cast<uint32_t>(r.x), static_cast<uint32_t>(r.y), static_cast<uint32_t>(r.z),
+         static_cast<uint32_t>(r.w)};
+  } else if constexpr (MODE == kNT) {
     v = __builtin_nontemporal_load((gload_t)(base + off));
-  else
+  } else {
     v = *(gload_t)(base + off);
+  }
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <bool NT = false>
-__device__ __forceinline__ void store16(uint64_t base, long long off, uint4 v) {
-  u32x4 w = {v.x, v.y, v.z, v.w};
-  if constexpr (NT)
-    __builtin_nontemporal_store(w, (gstore_t)(base + off));
-  else
-    *(gstore_t)(base + off) = w;
+template <int MODE = kPlain>
+__device__ __forceinline__ void store16(uint64_t base, long long off, uint4 v, int len = 0) {
+  if constexpr (MODE == kBufNT) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
+    const v4i w = {static_cast<int>(v.x), static_cast<int>(v.y), static_cast<int>(v.z),
+                   static_cast<int>(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, static_cast<int>(off), 0, 2 /* nt */);
+  } else {
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    if constexpr (MODE == kNT)
+      __builtin_nontemporal_store(w, (gstore_t)(base + off));
+    else
+      *(gstore_t)(base + off) = w;
+  }
 }
 
 // Tuning policy of the vector encode kernel (tools/ec_probe.hip explores others).
 //   U      sources whose loads are issued together before any arithmetic
-//   NT_LD  non-temporal source loads;  NT_ST  non-temporal parity stores
-//   ORDER  0: work item = (stripe, tile) with tile fastest; 1: stripe fastest
+//   LD/ST  memory access modes of source loads / parity stores (above)
+//   ORDER  0: work item = (stripe, tile) with tile fastest; 1: stripe fastest;
+//          2: XCD-contiguous
 // Measured on MI355X (profiles/r01_probe_variants_*.txt): non-temporal loads
-// AND stores lift the 10-read/4-write stream from 5.5 to 6.1 TB/s, and issuing
-// all of a stripe's source loads at once (U = k) adds ~1 %; the work order and
-// shard padding do not help. The library picks U from k at launch (enc_group).
-template <int UU>
-struct EncNT {
+// AND stores lift the 10-read/4-write stream from 5.5 to 6.1 TB/s, issuing
+// all of a stripe's source loads at once (U = k) adds ~1 %, buffer ops ~1 %;
+// the work order and shard padding do not help. The library picks U from k
+// at launch (enc_group).
+template <int UU, int LDM = kBufNT, int STM = kBufNT, int ORD = 0>
+struct EncPol {
   static constexpr int U = UU;
-  static constexpr bool NT_LD = true, NT_ST = true;
-  static constexpr int ORDER = 0;
+  static constexpr int LD = LDM, ST = STM;
+  static constexpr int ORDER = ORD;
 };
+template <int UU>
+using EncNT = EncPol<UU>;
 using EncDefault = EncNT<4>;
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -151,12 +176,13 @@ __device__ __forceinline__ void mac16x2(uint32_t (&acc)[P][4], const uint4& x, c
 // U sources j..j+U-1: issue all U loads before any arithmetic, then fold the
 // sources in pairs; the scheduling barriers keep one pair's temporaries live
 // at a time (otherwise the scheduler hoists every lookup and spills).
-template <int P, int U, bool NT = false>
+template <int P, int U, int MODE = kPlain>
 __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
-                                        int j, long long off, const uint32_t* __restrict__ tbl) {
+                                        int j, long long off, const uint32_t* __restrict__ tbl,
+                                        int len) {
   uint4 x[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) x[u] = load16<NT>(sp[j + u], off);
+  for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
   // Pairs share XOR3s but hold two sources' tables (2*P*5 SGPRs): only for P <= 4.
   constexpr int PAIR = P <= 4 ? 2 : 1;
 #pragma unroll
@@ -225,20 +251,21 @@ constexpr int enc_waves() {
 // acc[l] = XOR_j c[l][j] * src[j][off..off+16) for one lane.
 template <int P, class Pol>
 __device__ __forceinline__ void accum16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
-                                        const uint32_t* __restrict__ tbl, int k, long long off) {
+                                        const uint32_t* __restrict__ tbl, int k, long long off,
+                                        int len) {
 #pragma unroll
   for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
   int j = 0;
-  for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::NT_LD>(acc, src, j, off, tbl);
+  for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::LD>(acc, src, j, off, tbl, len);
   // Remainder. The launcher only picks U > 4 when U divides k, so there the
   // (cheap, correct for any k) single-source loop is dead in practice.
   if constexpr (Pol::U == 4) {
     if (j + 2 <= k) {
-      chunk16<P, 2, Pol::NT_LD>(acc, src, j, off, tbl);
+      chunk16<P, 2, Pol::LD>(acc, src, j, off, tbl, len);
       j += 2;
     }
   }
-  for (; j < k; ++j) chunk16<P, 1, Pol::NT_LD>(acc, src, j, off, tbl);
+  for (; j < k; ++j) chunk16<P, 1, Pol::LD>(acc, src, j, off, tbl, len);
 }
 
 template <int P, class Pol = EncDefault>
@@ -266,10 +293,11 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U>())) void ec_encode_v1
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
       uint32_t acc[P][4];
-      accum16<P, Pol>(acc, sp + src0, tbl, k, off);
+      accum16<P, Pol>(acc, sp + src0, tbl, k, off, len);
 #pragma unroll
       for (int l = 0; l < P; ++l)
-        store16<Pol::NT_ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]));
+        store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
+                         len);
     } else if (off < len) {
       dot_bytes<P>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off));
     }
@@ -308,10 +336,10 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, 4>())) void ec_verify_v16(
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
       uint32_t acc[P][4];
-      accum16<P, EncNT<4>>(acc, sp + src0, tbl, k, off);
+      accum16<P, EncNT<4>>(acc, sp + src0, tbl, k, off, len);
 #pragma unroll
       for (int l = 0; l < P; ++l) {
-        const uint4 e = load16<true>(sp[dst0 + l], off);
+        const uint4 e = load16<kBufNT>(sp[dst0 + l], off, len);
         const uint32_t x[4] = {acc[l][0] ^ e.x, acc[l][1] ^ e.y, acc[l][2] ^ e.z, acc[l][3] ^ e.w};
 #pragma unroll
         for (int d = 0; d < 4; ++d)
@@ -370,10 +398,10 @@ __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restri
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
-      const uint4 x = load16<true>(sp[src_idx], off);
+      const uint4 x = load16<kBufNT>(sp[src_idx], off, len);
       uint4 d[P];
 #pragma unroll
-      for (int l = 0; l < P; ++l) d[l] = load16<true>(sp[dst0 + l], off);
+      for (int l = 0; l < P; ++l) d[l] = load16<kBufNT>(sp[dst0 + l], off, len);
       const Sel s0 = split(x.x), s1 = split(x.y), s2 = split(x.z), s3 = split(x.w);
 #pragma unroll
       for (int l = 0; l < P; ++l) {
@@ -382,7 +410,7 @@ __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restri
         d[l].y ^= gf_mul4(c, s1);
         d[l].z ^= gf_mul4(c, s2);
         d[l].w ^= gf_mul4(c, s3);
-        store16<true>(sp[dst0 + l], off, d[l]);
+        store16<kBufNT>(sp[dst0 + l], off, d[l], len);
       }
     } else if (off < len) {
       mad_bytes<P>(sp, src_idx, dst0, tbl, off, static_cast<int>(len - off));

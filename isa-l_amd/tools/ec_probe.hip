@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void mem_pattern(const uint64_t* __restrict__ 
     uint4 a = make_uint4(w, 1, 2, 3);
     uint4 x[R > 0 ? R : 1];
 #pragma unroll
-    for (int j = 0; j < R; ++j) x[j] = load16<NT_LD>(sp[j], off);
+    for (int j = 0; j < R; ++j) x[j] = load16<NT_LD ? kNT : kPlain>(sp[j], off);
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       a.x ^= x[j].x;
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void mem_pattern(const uint64_t* __restrict__ 
     }
 #pragma unroll
     for (int l = 0; l < W; ++l) {
-      store16<NT_ST>(sp[10 + l], off, a);  // parity pointers (k = 10) only
+      store16<NT_ST ? kNT : kPlain>(sp[10 + l], off, a);  // parity pointers (k = 10) only
       a.x += 1;
     }
   }
@@ -109,8 +109,8 @@ __global__ __launch_bounds__(256) void mem_pattern_2t(const uint64_t* __restrict
     uint4 x0[R], x1[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      x0[j] = load16<true>(sp[j], off0);
-      x1[j] = load16<true>(sp[j], off0 + 1024);
+      x0[j] = load16<kNT>(sp[j], off0);
+      x1[j] = load16<kNT>(sp[j], off0 + 1024);
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -119,8 +119,8 @@ __global__ __launch_bounds__(256) void mem_pattern_2t(const uint64_t* __restrict
     }
 #pragma unroll
     for (int l = 0; l < W; ++l) {
-      store16<true>(sp[10 + l], off0, a0);
-      store16<true>(sp[10 + l], off0 + 1024, a1);
+      store16<kNT>(sp[10 + l], off0, a0);
+      store16<kNT>(sp[10 + l], off0 + 1024, a1);
       a0.x += 1;
       a1.x += 1;
     }
@@ -144,11 +144,7 @@ __global__ void fill_random(uint32_t* p, size_t n, uint32_t seed) {
 }
 
 template <int UU, bool NL, bool NS, int ORD>
-struct Pol {
-  static constexpr int U = UU;
-  static constexpr bool NT_LD = NL, NT_ST = NS;
-  static constexpr int ORDER = ORD;
-};
+using Pol = EncPol<UU, NL ? kNT : kPlain, NS ? kNT : kPlain, ORD>;
 
 struct Variant {
   std::string name;
@@ -265,20 +261,18 @@ int main(int argc, char** argv) {
                }});                                                                           \
   V.back().encode = true;
   using PNB = Pol<4, true, true, 0>;
-  using PNB2 = Pol<2, true, true, 0>;
-  using PNB5 = Pol<5, true, true, 0>;
   using PNB10 = Pol<10, true, true, 0>;
-  using PNBX = Pol<4, true, true, 2>;
   using PNB10X = Pol<10, true, true, 2>;
-  using PX = Pol<4, false, false, 2>;
-  ENC(EncDefault, 0, "encode default (U4)")
+  using PBUF10 = EncPol<10, kBufNT, kBufNT, 0>;
+  using PBUF10X = EncPol<10, kBufNT, kBufNT, 2>;
+  using PBUF5 = EncPol<5, kBufNT, kBufNT, 0>;
+  ENC(EncDefault, 0, "encode default (buf U4)")
   ENC(PNB, 0, "encode U4 nt-both")
-  ENC(PNB2, 0, "encode U2 nt-both")
-  ENC(PNB5, 0, "encode U5 nt-both")
   ENC(PNB10, 0, "encode U10 nt-both")
-  ENC(PNBX, 0, "encode U4 nt-both xcd-contig")
   ENC(PNB10X, 0, "encode U10 nt-both xcd-contig")
-  ENC(PX, 0, "encode U4 xcd-contig")
+  ENC(PBUF10, 0, "encode U10 buf-nt")
+  ENC(PBUF10X, 0, "encode U10 buf-nt xcd-contig")
+  ENC(PBUF5, 0, "encode U5 buf-nt")
 #define ENCP(POL, Q, NAME)                                                                     \
   V.push_back({NAME, enc_bytes, [=](hipStream_t st) {                                          \
                  hipLaunchKernelGGL((ec_encode_v16<4, POL>), dim3(nitems), dim3(256), 0, st,     \
