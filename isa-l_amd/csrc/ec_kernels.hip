@@ -199,8 +199,10 @@ __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* _
   }
 }
 
-// First-mismatch record of the verify kernels: key = column << 8 | row, kept
-// as the minimum over the launch (smallest column, then smallest row there).
+// First-mismatch record of the verify kernels: key = column << 8 | row. Each
+// workgroup keeps the minimum of its keys in an LDS word (ds_min_u64) and
+// writes it to its own slot at the end, so the result needs no device-scope
+// atomic and may live in pinned host memory (zero-copy small calls).
 __device__ __forceinline__ void note_mismatch(unsigned long long* bad, long long col, int row) {
   atomicMin(bad, (static_cast<unsigned long long>(col) << 8) | static_cast<unsigned>(row));
 }
@@ -328,7 +330,10 @@ template <int P>
 __global__ __launch_bounds__(kBlock, (enc_waves<P, 4>())) void ec_verify_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles,
-    unsigned long long* __restrict__ bad, int row0, long long col0) {
+    unsigned long long* __restrict__ slots, int row0, long long col0) {
+  __shared__ unsigned long long blk_min;
+  if (threadIdx.x == 0) blk_min = ~0ull;
+  __syncthreads();
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned stripe = w / tiles;
     const unsigned tile = w - stripe * tiles;
@@ -344,14 +349,17 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, 4>())) void ec_verify_v16(
 #pragma unroll
         for (int d = 0; d < 4; ++d)
           if (x[d]) {
-            note_mismatch(bad, col0 + off + 4 * d + (__builtin_ctz(x[d]) >> 3), row0 + l);
+            note_mismatch(&blk_min, col0 + off + 4 * d + (__builtin_ctz(x[d]) >> 3), row0 + l);
             break;
           }
       }
     } else if (off < len) {
-      dot_bytes<P, true>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off), bad, row0, col0);
+      dot_bytes<P, true>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off), &blk_min, row0,
+                         col0);
     }
   }
+  __syncthreads();
+  if (threadIdx.x == 0) slots[blockIdx.x] = blk_min;
 }
 
 template <int P>
@@ -359,15 +367,20 @@ __global__ __launch_bounds__(kBlock) void ec_verify_b1(const uint64_t* __restric
                                                        int ptr_stride, int src0, int dst0,
                                                        const uint32_t* __restrict__ tbl, int len,
                                                        int k, unsigned nitems, unsigned tiles,
-                                                       unsigned long long* __restrict__ bad,
+                                                       unsigned long long* __restrict__ slots,
                                                        int row0, long long col0) {
+  __shared__ unsigned long long blk_min;
+  if (threadIdx.x == 0) blk_min = ~0ull;
+  __syncthreads();
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned stripe = w / tiles;
     const unsigned tile = w - stripe * tiles;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kBlock + threadIdx.x;
-    if (off < len) dot_bytes<P, true>(sp, src0, dst0, tbl, k, off, 1, bad, row0, col0);
+    if (off < len) dot_bytes<P, true>(sp, src0, dst0, tbl, k, off, 1, &blk_min, row0, col0);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) slots[blockIdx.x] = blk_min;
 }
 
 // ---------------------------------------------------------------------------
@@ -546,30 +559,33 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
 
 extern "C" int isal_hip_launch_verify(const uint64_t* d_ptrs, int ptr_stride, int src_idx0,
                                       int dst_idx0, const uint32_t* d_tbl, int len, int k, int rows,
-                                      long long col0, unsigned long long* d_bad, int vec16,
-                                      void* stream) {
+                                      long long col0, unsigned long long* slots, int* nslots,
+                                      int vec16, void* stream) {
+  *nslots = 0;
   if (len <= 0 || rows <= 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned span = vec16 ? kTile : kBlock;
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
+  const unsigned grid = tiles < EC_VERIFY_MAX_GRID ? tiles : EC_VERIFY_MAX_GRID;
   for (int r0 = 0; r0 < rows; r0 += EC_MAX_ROWS_PER_PASS) {
     const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
     const uint32_t* tbl = d_tbl + static_cast<size_t>(kTbl) * k * r0;
     const int dst0 = dst_idx0 + r0;
-    const unsigned grid = grid_for(tiles);
+    unsigned long long* out = slots + *nslots;
     switch (P) {
 #define EC_CASE(n)                                                                            \
   case n:                                                                                     \
     if (vec16)                                                                                \
       hipLaunchKernelGGL(ec_verify_v16<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride, \
-                         src_idx0, dst0, tbl, len, k, tiles, tiles, d_bad, r0, col0);         \
+                         src_idx0, dst0, tbl, len, k, tiles, tiles, out, r0, col0);           \
     else                                                                                      \
       hipLaunchKernelGGL(ec_verify_b1<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride,  \
-                         src_idx0, dst0, tbl, len, k, tiles, tiles, d_bad, r0, col0);         \
+                         src_idx0, dst0, tbl, len, k, tiles, tiles, out, r0, col0);           \
     break;
       EC_CASE(1) EC_CASE(2) EC_CASE(3) EC_CASE(4) EC_CASE(5) EC_CASE(6) EC_CASE(7) EC_CASE(8)
 #undef EC_CASE
     }
+    *nslots += static_cast<int>(grid);
     isal_hip_count_launch();
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);

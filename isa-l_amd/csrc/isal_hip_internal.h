@@ -48,11 +48,16 @@ int isal_hip_launch_update(const uint64_t *d_ptrs, int ptr_stride, int src_idx, 
                            long long nstripes, int vec16, void *stream);
 
 /* Verify one stripe (nstripes = 1): recompute rows outputs from the sources and
- * compare with the bytes at the output pointers; *d_bad (preset to ~0 by the
- * caller) receives min((col0 + column) << 8 | row) over mismatches. */
+ * compare with the bytes at the output pointers. Each workgroup writes the
+ * minimum key (col0 + column) << 8 | row of its mismatches (~0 if none) to
+ * its own slot; *nslots receives the number of slots written (at most
+ * EC_VERIFY_SLOTS(rows)); the caller takes the minimum. */
+#define EC_VERIFY_MAX_GRID 2048
+#define EC_VERIFY_SLOTS(rows) \
+        ((((rows) + EC_MAX_ROWS_PER_PASS - 1) / EC_MAX_ROWS_PER_PASS) * EC_VERIFY_MAX_GRID)
 int isal_hip_launch_verify(const uint64_t *d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
                            const uint32_t *d_tbl, int len, int k, int rows, long long col0,
-                           unsigned long long *d_bad, int vec16, void *stream);
+                           unsigned long long *slots, int *nslots, int vec16, void *stream);
 
 /* The shim's generic synchronous call (host or device shard pointers).
  * op: ISAL_HIP_OP_ENCODE (dst = coded sources, nsrc = k), ISAL_HIP_OP_UPDATE

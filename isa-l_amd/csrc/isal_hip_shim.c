@@ -87,7 +87,8 @@ typedef struct {
         int device;
         hipStream_t stream;
         void *d_args; /* device: pointer table + coefficient tables */
-        void *h_args; /* pinned mirror of d_args */
+        void *h_args; /* pinned mirror of d_args (fine-grained, coherent) */
+        void *h_args_dev; /* the same pinned buffer as seen by kernels (zero-copy) */
         size_t args_cap;
         unsigned char *d_stage; /* device scratch for host-resident shards */
         size_t stage_cap;
@@ -161,9 +162,13 @@ ensure_args(ctx_t *c, size_t bytes)
                 HIP_OR_DIE(hipFree(c->d_args));
         if (c->h_args)
                 HIP_OR_DIE(hipHostFree(c->h_args));
-        c->d_args = c->h_args = NULL;
+        c->d_args = c->h_args = c->h_args_dev = NULL;
         HIP_OR_DIE(hipMalloc(&c->d_args, cap));
-        HIP_OR_DIE(hipHostMalloc(&c->h_args, cap, hipHostMallocDefault));
+        /* coherent: kernels of the zero-copy path read arguments and shards the
+         * host just wrote, and the host reads what they wrote, with no cached
+         * copies in between */
+        HIP_OR_DIE(hipHostMalloc(&c->h_args, cap, hipHostMallocCoherent));
+        HIP_OR_DIE(hipHostGetDevicePointer(&c->h_args_dev, c->h_args, 0));
         c->args_cap = cap;
 }
 
@@ -213,44 +218,103 @@ on_device(const void *p)
 
 enum { OP_ENCODE = ISAL_HIP_OP_ENCODE, OP_UPDATE = ISAL_HIP_OP_UPDATE, OP_VERIFY = ISAL_HIP_OP_VERIFY };
 
-/* Host-staged calls up to this many staged bytes are packed through the pinned
- * argument buffer (one H2D + one D2H DMA per call instead of one pageable copy
- * per shard): the reference's own tests make ~10^5 such calls of a few KiB. */
-#define SMALL_STAGE_BYTES ((size_t) 4 << 20)
+/*
+ * Three ways to run one synchronous call, by size:
+ *   zero-copy  len * (k + rows) <= ZC_BYTES: pointer table, coefficient tables,
+ *              host-resident shards and verify slots all live in the pinned
+ *              buffer and the kernel reads/writes them over PCIe — the call is
+ *              one launch and one stream sync;
+ *   packed     host-staged bytes <= PACK_BYTES: the same layout, moved with one
+ *              H2D and one D2H DMA into/out of HBM;
+ *   chunked    larger: shards staged per column chunk (run_ec below).
+ * The reference's own tests make ~10^5-10^7 calls of a few KiB each.
+ */
+#define ZC_BYTES ((size_t) 256 << 10)
+#define PACK_BYTES ((size_t) 4 << 20)
 
-static void launch_op(ctx_t *c, int op, size_t ptr_bytes, size_t args_bytes, int nptr, int nsrc,
-                      int clen, long long c0, int k, int rows, int vec_i, int vec16);
+/* Byte layout of the argument buffer of one call. */
+typedef struct {
+        size_t ptr_bytes, args_bytes, slots_off, slots_bytes, stage_off, slot, total;
+} layout_t;
 
+static layout_t
+call_layout(int op, int len, int k, int rows, int nptr, int nstage)
+{
+        layout_t L;
+        L.ptr_bytes = ((size_t) nptr * 8 + 15) & ~(size_t) 15;
+        L.args_bytes = L.ptr_bytes + ((isal_hip_tables_dwords(k, rows) * 4 + 15) & ~(size_t) 15);
+        L.slots_off = L.args_bytes;
+        L.slots_bytes = op == OP_VERIFY ? (size_t) EC_VERIFY_SLOTS(rows) * 8 : 0;
+        L.stage_off = (L.slots_off + L.slots_bytes + 255) & ~(size_t) 255;
+        L.slot = ((size_t) len + 255) & ~(size_t) 255;
+        L.total = L.stage_off + L.slot * (size_t) nstage;
+        return L;
+}
+
+static unsigned long long
+min_slot(const unsigned long long *slots, int n)
+{
+        unsigned long long m = ~0ull;
+        int i;
+        for (i = 0; i < n; i++)
+                if (slots[i] < m)
+                        m = slots[i];
+        return m;
+}
+
+/* Enqueue one chunk's kernel(s) with the argument block at `args` (device or
+ * zero-copy view). For OP_VERIFY returns the number of slots written at
+ * args + L->slots_off. */
+static int
+launch_op(ctx_t *c, int op, char *args, const layout_t *L, int nptr, int nsrc, int clen,
+          long long c0, int k, int rows, int vec_i, int vec16)
+{
+        const uint64_t *ptrs = (const uint64_t *) args;
+        const uint32_t *tbl = (const uint32_t *) (args + L->ptr_bytes);
+        int err, nslots = 0;
+        if (op == OP_VERIFY)
+                err = isal_hip_launch_verify(ptrs, nptr, 0, nsrc, tbl, clen, k, rows, c0,
+                                             (unsigned long long *) (args + L->slots_off), &nslots,
+                                             vec16, c->stream);
+        else if (op == OP_ENCODE)
+                err = isal_hip_launch_encode(ptrs, nptr, 0, nsrc, tbl, clen, k, rows, 1, vec16,
+                                             c->stream);
+        else
+                err = isal_hip_launch_update(ptrs, nptr, 0, nsrc, tbl, clen, k, rows, vec_i, 1,
+                                             vec16, c->stream);
+        if (err)
+                die("kernel launch", (hipError_t) err);
+        return nslots;
+}
+
+/* zero-copy and packed modes (whole shards, one chunk) */
 static unsigned long long
 run_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
           unsigned char *const *src, int nsrc, unsigned char *const *dst, const int *flag,
-          int nstage)
+          int nstage, int zero_copy)
 {
-        int nptr = nsrc + rows, i, s, first_out = -1, vec16 = 1;
-        size_t slot = ((size_t) len + 255) & ~(size_t) 255;
-        size_t tbl_dwords = isal_hip_tables_dwords(k, rows);
-        size_t ptr_bytes = ((size_t) nptr * 8 + 15) & ~(size_t) 15;
-        size_t args_bytes = ptr_bytes + ((tbl_dwords * 4 + 15) & ~(size_t) 15);
-        size_t stage_off = args_bytes + 16, upload = stage_off;
-        unsigned char *hs, *ds;
+        int nptr = nsrc + rows, i, s, first_out = -1, vec16 = 1, nslots;
+        layout_t L = call_layout(op, len, k, rows, nptr, nstage);
+        char *h, *dv;
+        size_t upload;
         uint64_t *h_ptrs;
-        unsigned long long first_bad = ~0ull;
 
-        ensure_args(c, stage_off + slot * (size_t) nstage);
-        h_ptrs = (uint64_t *) c->h_args;
-        isal_hip_build_tables(k, rows, gftbls, (uint32_t *) ((char *) c->h_args + ptr_bytes));
-        hs = (unsigned char *) c->h_args + stage_off;
-        ds = (unsigned char *) c->d_args + stage_off;
+        ensure_args(c, L.total);
+        h = (char *) c->h_args;
+        dv = zero_copy ? (char *) c->h_args_dev : (char *) c->d_args; /* what kernels see */
+        h_ptrs = (uint64_t *) h;
+        isal_hip_build_tables(k, rows, gftbls, (uint32_t *) (h + L.ptr_bytes));
+        upload = L.args_bytes;
         for (i = 0, s = 0; i < nptr; i++) {
                 unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
                 uint64_t d;
                 if (flag[i]) {
                         d = (uint64_t) (uintptr_t) host;
                 } else {
-                        d = (uint64_t) (uintptr_t) (ds + (size_t) s * slot);
+                        d = (uint64_t) (uintptr_t) (dv + L.stage_off + (size_t) s * L.slot);
                         if (i < nsrc || op != OP_ENCODE) {
-                                memcpy(hs + (size_t) s * slot, host, (size_t) len);
-                                upload = stage_off + (size_t) (s + 1) * slot;
+                                memcpy(h + L.stage_off + (size_t) s * L.slot, host, (size_t) len);
+                                upload = L.stage_off + (size_t) (s + 1) * L.slot;
                         }
                         if (i >= nsrc && first_out < 0)
                                 first_out = s;
@@ -260,54 +324,28 @@ run_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
                 if (d & 15)
                         vec16 = 0;
         }
-        memset((char *) c->h_args + args_bytes, 0xff, 8);
-        HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, upload, hipMemcpyHostToDevice, c->stream));
-        launch_op(c, op, ptr_bytes, args_bytes, nptr, nsrc, len, 0, k, rows, vec_i, vec16);
-        if (op != OP_VERIFY && first_out >= 0)
-                HIP_OR_DIE(hipMemcpyAsync(hs + (size_t) first_out * slot, ds + (size_t) first_out * slot,
-                                          (size_t) (nstage - first_out) * slot, hipMemcpyDeviceToHost,
-                                          c->stream));
-        HIP_OR_DIE(hipStreamSynchronize(c->stream));
-        if (op == OP_VERIFY) {
-                memcpy(&first_bad, (char *) c->h_args + args_bytes, 8);
-                return first_bad;
+        if (!zero_copy)
+                HIP_OR_DIE(hipMemcpyAsync(c->d_args, h, upload, hipMemcpyHostToDevice, c->stream));
+        nslots = launch_op(c, op, dv, &L, nptr, nsrc, len, 0, k, rows, vec_i, vec16);
+        if (!zero_copy) {
+                if (op == OP_VERIFY)
+                        HIP_OR_DIE(hipMemcpyAsync(h + L.slots_off, (char *) c->d_args + L.slots_off,
+                                                  (size_t) nslots * 8, hipMemcpyDeviceToHost,
+                                                  c->stream));
+                else if (first_out >= 0)
+                        HIP_OR_DIE(hipMemcpyAsync(h + L.stage_off + (size_t) first_out * L.slot,
+                                                  (char *) c->d_args + L.stage_off +
+                                                          (size_t) first_out * L.slot,
+                                                  (size_t) (nstage - first_out) * L.slot,
+                                                  hipMemcpyDeviceToHost, c->stream));
         }
+        HIP_OR_DIE(hipStreamSynchronize(c->stream));
+        if (op == OP_VERIFY)
+                return min_slot((const unsigned long long *) (h + L.slots_off), nslots);
         for (i = nsrc, s = first_out; i < nptr && s >= 0; i++)
                 if (!flag[i])
-                        memcpy(dst[i - nsrc], hs + (size_t) s++ * slot, (size_t) len);
-        return first_bad;
-}
-
-/* Enqueue the kernel(s) of one chunk on c->stream; for OP_VERIFY the result
- * word (at d_args + args_bytes, uploaded as ~0) is copied back to the same
- * offset of the pinned buffer. */
-static void
-launch_op(ctx_t *c, int op, size_t ptr_bytes, size_t args_bytes, int nptr, int nsrc, int clen,
-          long long c0, int k, int rows, int vec_i, int vec16)
-{
-        const uint64_t *d_ptrs = (const uint64_t *) c->d_args;
-        const uint32_t *d_tbl = (const uint32_t *) ((char *) c->d_args + ptr_bytes);
-        int err;
-        if (op == OP_VERIFY) {
-                /* the result word was preset to ~0 in the pinned buffer and
-                 * arrived with the argument upload */
-                unsigned long long *d_bad = (unsigned long long *) ((char *) c->d_args + args_bytes);
-                err = isal_hip_launch_verify(d_ptrs, nptr, 0, nsrc, d_tbl, clen, k, rows, c0, d_bad,
-                                             vec16, c->stream);
-                if (err)
-                        die("kernel launch", (hipError_t) err);
-                HIP_OR_DIE(hipMemcpyAsync((char *) c->h_args + args_bytes, d_bad, 8,
-                                          hipMemcpyDeviceToHost, c->stream));
-                return;
-        }
-        if (op == OP_ENCODE)
-                err = isal_hip_launch_encode(d_ptrs, nptr, 0, nsrc, d_tbl, clen, k, rows, 1, vec16,
-                                             c->stream);
-        else
-                err = isal_hip_launch_update(d_ptrs, nptr, 0, nsrc, d_tbl, clen, k, rows, vec_i, 1,
-                                             vec16, c->stream);
-        if (err)
-                die("kernel launch", (hipError_t) err);
+                        memcpy(dst[i - nsrc], h + L.stage_off + (size_t) s++ * L.slot, (size_t) len);
+        return ~0ull;
 }
 
 /*
@@ -325,10 +363,10 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         ctx_t *c;
         int nptr = nsrc + rows, i, nstage = 0;
         int dev_flag[512];
-        int *flag;
-        size_t tbl_dwords, ptr_bytes, args_bytes, chunk, slot;
+        int *flag, nslots;
+        size_t chunk, slot;
+        layout_t L;
         uint64_t *h_ptrs;
-        uint32_t *h_tbl;
         long long c0;
 
         if (len <= 0 || rows <= 0 || k < 0)
@@ -353,9 +391,11 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 nstage += !flag[i];
         }
 
-        if (nstage && (size_t) len * (size_t) nstage <= SMALL_STAGE_BYTES) {
-                unsigned long long r = run_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst,
-                                                 flag, nstage);
+        if ((size_t) len * (size_t) nptr <= ZC_BYTES ||
+            (nstage && (size_t) len * (size_t) nstage <= PACK_BYTES)) {
+                unsigned long long r =
+                        run_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage,
+                                  (size_t) len * (size_t) nptr <= ZC_BYTES);
                 if (flag != dev_flag)
                         free(flag);
                 return r;
@@ -375,13 +415,10 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 slot = 0;
         }
 
-        tbl_dwords = isal_hip_tables_dwords(k, rows);
-        ptr_bytes = ((size_t) nptr * 8 + 15) & ~(size_t) 15;
-        args_bytes = ptr_bytes + ((tbl_dwords * 4 + 15) & ~(size_t) 15);
-        ensure_args(c, args_bytes + 16); /* + the verify result word */
+        L = call_layout(op, len, k, rows, nptr, 0);
+        ensure_args(c, L.stage_off);
         h_ptrs = (uint64_t *) c->h_args;
-        h_tbl = (uint32_t *) ((char *) c->h_args + ptr_bytes);
-        isal_hip_build_tables(k, rows, gftbls, h_tbl);
+        isal_hip_build_tables(k, rows, gftbls, (uint32_t *) ((char *) c->h_args + L.ptr_bytes));
 
         for (c0 = 0; c0 < len; c0 += (long long) chunk) {
                 int clen = (int) ((long long) len - c0 < (long long) chunk ? len - c0 : (long long) chunk);
@@ -404,13 +441,19 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                         if (d & 15)
                                 vec16 = 0;
                 }
-                memset((char *) c->h_args + args_bytes, 0xff, 8);
-                HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, args_bytes + 16,
+                HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, L.args_bytes,
                                           hipMemcpyHostToDevice, c->stream));
-                launch_op(c, op, ptr_bytes, args_bytes, nptr, nsrc, clen, c0, k, rows, vec_i, vec16);
+                nslots = launch_op(c, op, (char *) c->d_args, &L, nptr, nsrc, clen, c0, k, rows,
+                                   vec_i, vec16);
                 if (op == OP_VERIFY) {
+                        HIP_OR_DIE(hipMemcpyAsync((char *) c->h_args + L.slots_off,
+                                                  (char *) c->d_args + L.slots_off,
+                                                  (size_t) nslots * 8, hipMemcpyDeviceToHost,
+                                                  c->stream));
                         HIP_OR_DIE(hipStreamSynchronize(c->stream));
-                        memcpy(&first_bad, (char *) c->h_args + args_bytes, 8);
+                        first_bad = min_slot(
+                                (const unsigned long long *) ((char *) c->h_args + L.slots_off),
+                                nslots);
                         if (first_bad != ~0ull)
                                 break;
                         continue;
