@@ -50,7 +50,8 @@ def parse_args(argv=None):
     ap.add_argument("--p", type=int, default=4)
     ap.add_argument("--len", type=int, default=1 << 20, help="shard bytes")
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU per step")
-    ap.add_argument("--workload", choices=["encode", "decode", "update", "e2e-update", "e2e-encode"],
+    ap.add_argument("--workload", choices=["encode", "decode", "update", "encode-crc", "crc",
+                                           "e2e-update", "e2e-encode"],
                     default="encode",
                     help="e2e-*: host-resident (pinned) stripes streamed through the pipeline")
     ap.add_argument("--depth", type=int, default=3, help="e2e pipeline depth (stripes in flight)")
@@ -182,7 +183,10 @@ def pmc_traffic(workload, k, p, n, S, kernel):
     import statistics
 
     want = {"workload": workload, "k": str(k), "p": str(p), "len": str(n), "stripes": str(S)}
-    name = kernel.split("<")[0] + "<" + kernel.split("<")[1].split(">")[0].split(",")[0]
+    def norm(x):
+        return x.replace("(anonymous namespace)::", "").replace(" ", "")
+
+    name = "void" + norm(kernel)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_*.csv")), reverse=True):
         with open(path) as f:
             lines = f.read().splitlines()
@@ -192,9 +196,8 @@ def pmc_traffic(workload, k, p, n, S, kernel):
             continue
         vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
         for l in lines:
-            parts = l.split(",")
-            if len(parts) >= 4 and parts[0] in vals and parts[3].replace(" ", "").startswith(
-                    "void" + name.replace(" ", "")):
+            parts = l.split(",", 3)
+            if len(parts) == 4 and parts[0] in vals and norm(parts[3]).split("(")[0] == name:
                 vals[parts[0]].append(float(parts[2]))
         if vals["FETCH_SIZE"] and vals["WRITE_SIZE"]:
             kib = 2 * statistics.median(vals["FETCH_SIZE"]) + statistics.median(vals["WRITE_SIZE"])
@@ -206,7 +209,7 @@ def pmc_traffic(workload, k, p, n, S, kernel):
 # CPU baseline: the reference's own ec_encode_data on this host
 # ---------------------------------------------------------------------------
 
-def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference"):
+def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=False, encode=True):
     """Times the reference ec_encode_data (oracle/_ref/libisal_ref.so: ec_base.c +
     ec_base_aliases.c compiled from /root/reference) on `threads` host threads,
     each encoding its own k x n stripe repeatedly for ~`seconds`.
@@ -245,6 +248,26 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference"):
     u8p = ctypes.POINTER(ctypes.c_ubyte)
     enc.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.POINTER(u8p), ctypes.POINTER(u8p)]
     enc.restype = None
+    crc_fn = None
+    if crc:
+        # + crc32_iscsi of every shard: the reference's crc_base.c when built
+        # (oracle/_ref/libisal_ref_crc.so), else the oracle restatement of it
+        cref = os.path.join(REPO, "oracle", "_ref", "libisal_ref_crc.so")
+        if impl == "gfni":  # SSE4.2 crc32q, 3 streams (as crc32_iscsi_01.asm)
+            crc_fn = G.gfni_port_crc32_iscsi
+            crc_fn.argtypes = [u8p, ctypes.c_longlong, ctypes.c_uint]
+        elif kind == "reference" and os.path.exists(cref):
+            crc_fn = ctypes.CDLL(cref).crc32_iscsi_base
+            crc_fn.argtypes = [u8p, ctypes.c_int, ctypes.c_uint]
+        else:
+            crc_fn = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so")).oracle_crc32_iscsi
+            crc_fn.argtypes = [u8p, ctypes.c_longlong, ctypes.c_uint]
+        crc_fn.restype = ctypes.c_uint
+        crc_what = ("crc32_iscsi of all k+p shards (" +
+                    ("SSE4.2 port of crc32_iscsi_01" if impl == "gfni" else "crc_base.c") + ")")
+        what = f"ec_encode_data from {what} + {crc_what}" if encode else crc_what
+    else:
+        what = f"ec_encode_data from {what}"
 
     a = np.zeros((k + p) * k, np.uint8)
     gen(a.ctypes.data_as(u8p), k + p, k)
@@ -273,8 +296,13 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference"):
     def worker(i):
         src, dst = ptrs(bufs[i][0]), ptrs(bufs[i][1])
         t = tbls.ctypes.data_as(u8p)
+        shards = [b.ctypes.data_as(u8p) for b in bufs[i][0] + bufs[i][1]]
         while time.perf_counter() < deadline:
-            enc(n, k, p, t, src, dst)  # ctypes drops the GIL for the call
+            if encode:
+                enc(n, k, p, t, src, dst)  # ctypes drops the GIL for the call
+            if crc_fn is not None:
+                for sh in shards:
+                    crc_fn(sh, n, 0xFFFFFFFF)
             counts[i] += 1
 
     t0 = time.perf_counter()
@@ -288,7 +316,7 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference"):
         "unit": "GiB/s",
         "cores": threads,
         "kind": kind,
-        "sample": f"{stripes} stripes of k={k} p={p} x {n} B, ec_encode_data from {what}, "
+        "sample": f"{stripes} stripes of k={k} p={p} x {n} B, {what}, "
                   f"{threads} threads x {wall:.1f} s",
         "parity_stripe_match": parity_ok,
     }
@@ -347,7 +375,7 @@ def main(argv=None):
                                [int(frag(s, i).data_ptr()) for s in range(S) for i in surv],
                                [int(out[s, i].data_ptr()) for s in range(S) for i in range(rows)])
         bytes_per_launch = (k + rows) * n * S
-        kernel = f"ec_encode_v16<{rows}, EncNT<{enc_group(k)}>>"
+        kernel = f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, 2, 2, 0>>"
         workload = f"C3 decode: recover data shards {errs} of k={k} p={p} RS, {n} B shards x {S} stripes/GPU"
     else:
         rows = p
@@ -356,8 +384,22 @@ def main(argv=None):
                                [int(out[s, l].data_ptr()) for s in range(S) for l in range(p)])
         if args.workload == "encode":
             bytes_per_launch = (k + p) * n * S
-            kernel = f"ec_encode_v16<{p}, EncNT<{enc_group(k)}>>"
+            kernel = f"ec_encode_v16<{p}, EncPol<{enc_group(k)}, 2, 2, 0>>"
             workload = f"C2 encode: k={k} p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU"
+        elif args.workload in ("encode-crc", "crc"):
+            # fragment checksums: crc32_iscsi of all k+p shards,
+            # fused into the encode pass or as a checksum-only pass
+            crc_out = torch.zeros(S * (k + p), dtype=torch.int32, device=dev)
+            bytes_per_launch = (k + p) * n * S
+            if args.workload == "encode-crc":
+                kernel = f"ec_encode_crc_v16<{p}, EncPol<{enc_group(k)}, 2, 2, 0>>"
+                workload = (f"C2 encode + CRC32C (crc32_iscsi) of all k+p shards in one pass: k={k} "
+                            f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
+            else:
+                batch.encode(torch.cuda.current_stream(dev).cuda_stream)
+                kernel = "crc32c_shards<true>"
+                workload = (f"CRC32C (crc32_iscsi) of all k+p={k + p} shards, {n} B x {S} "
+                            f"stripes/GPU, device-resident")
         else:
             bytes_per_launch = (1 + 2 * p) * n * S
             kernel = f"ec_update_v16<{p}>"
@@ -372,6 +414,10 @@ def main(argv=None):
         if args.workload == "update":
             batch.update(vec[0] % k, h)
             vec[0] += 1
+        elif args.workload == "encode-crc":
+            batch.encode_crc(0xFFFFFFFF, crc_out, h)
+        elif args.workload == "crc":
+            batch.crc(0xFFFFFFFF, crc_out, h)
         else:
             batch.encode(h)
 
@@ -397,7 +443,16 @@ def main(argv=None):
     # is all ones, so it must equal the XOR of the sources; decode must return
     # exactly the erased shards. Reduced with MIN over ranks.
     ok = True
-    if args.workload == "encode":
+    if args.workload in ("encode-crc", "crc"):
+        # the fused kernel and the checksum-only kernel must agree on every shard
+        crc_ref = torch.zeros_like(crc_out)
+        if args.workload == "encode-crc":
+            batch.crc(0xFFFFFFFF, crc_ref, h)
+        else:
+            batch.encode_crc(0xFFFFFFFF, crc_ref, h)
+        torch.cuda.synchronize(dev)
+        ok &= bool(torch.equal(crc_ref, crc_out))
+    if args.workload in ("encode", "encode-crc"):
         for s_ in sorted({0, S // 2, S - 1}):
             x = data[s_, 0].clone()
             for j in range(1, k):
@@ -458,13 +513,16 @@ def main(argv=None):
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         check = None
-        if args.workload == "encode":
+        if args.workload in ("encode", "encode-crc"):
             check = (data[0].cpu().numpy(), out[0].cpu().numpy())
-        result["cpu_baseline"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check)
+        with_crc = args.workload in ("encode-crc", "crc")
+        only_crc = args.workload == "crc"
+        result["cpu_baseline"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check, crc=with_crc,
+                                              encode=not only_crc)
         # the reference's fast x86 path cannot be assembled here (no nasm): its
         # AVX-512+GFNI kernels restated in C intrinsics, timed the same way
         result["cpu_baseline_simd_port"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check,
-                                                        impl="gfni")
+                                                        impl="gfni", crc=with_crc, encode=not only_crc)
     else:
         result["cpu_baseline"] = None
     if d.rank == 0:

@@ -54,6 +54,27 @@ int isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream);
 
 int isal_hip_batch_destroy(isal_hip_batch *b);
 
+/*
+ * Fragment checksums (the step storage callers run right after
+ * encoding). crc receives nstripes*(k+rows) values in DEVICE memory:
+ *   crc[s*(k+rows) + j]     = crc32_iscsi(data[s*k + j],   len, init)  (j < k)
+ *   crc[s*(k+rows) + k + l] = crc32_iscsi(coding[s*rows + l], len, init)
+ * with the reference's crc32_iscsi semantics (include/crc.h:137-141,
+ * crc/crc_base.c:205-219: reflected CRC32C, register starts at init, no final
+ * inversion).
+ *
+ * isal_hip_batch_encode_crc: ec_encode_data for every stripe AND the checksums
+ *   of the sources and the fresh parity, in one pass over HBM when the shards
+ *   are 16-byte aligned, len % 16 == 0 and k <= 64 (otherwise encode, then a
+ *   checksum pass).
+ * isal_hip_batch_crc: checksums only (e.g. to verify fragments read back).
+ * The first call allocates the per-lane partials: nstripes*(k+rows) *
+ * ceil(len/65536) KiB of device memory (~1/64 of the shard bytes).
+ */
+int isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc,
+                              void *stream);
+int isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream);
+
 /* ---- streaming pipeline for HOST-resident stripes ----------------------- */
 
 /*

@@ -1,0 +1,428 @@
+// crc_kernels.hip — CRC32C (the reference's crc32_iscsi, crc/crc_base.c:205-219)
+// of erasure-code shards on gfx950, standalone and fused into the encode pass.
+//
+// storage callers checksum every fragment right after
+// encoding (include/crc.h:137). Reading the k sources and writing the parity a
+// second time just to checksum them would double the HBM traffic of the stripe,
+// so the fused kernel computes the CRCs of all k + rows shards from the same
+// registers the encode already holds.
+//
+// Algorithm (GF(2)-linear CRC, constants from crc_host.c):
+//  * lane L of a workgroup owns bytes [16L, 16L+16) of each 4 KiB tile (the
+//    encode kernel's layout); crc(0, chunk) = XOR_i T_{15-i}[b_i] with 16 slice
+//    tables in LDS (one ds_read_b32 per byte);
+//  * across the workgroup's `tt` consecutive tiles the lane chains its chunks:
+//    a = Z^4096(a) ^ crc(0, chunk)  (four byte-table lookups);
+//  * the lane's chain is a partial (part[], 1 dword per 16*tt bytes: 0.4 % extra
+//    writes at tt = 16); crc32c_combine joins the partials of a shard with
+//    Horner across workgroups, one multiply per lane to the shard end and a
+//    block XOR-reduction, then adds Z^len(init_crc).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ec_device.h"
+
+namespace {
+
+constexpr uint32_t kCrcPoly = 0x82F63B78u;
+constexpr int kCrcTabDw = ISAL_HIP_CRC_TAB_DWORDS;
+constexpr int kShiftTab = ISAL_HIP_CRC_SLICES * 256;  // Z^4096 byte tables follow the slices
+static_assert(ISAL_HIP_CRC_TILE == kTile, "CRC tile = encode tile");
+
+__device__ __forceinline__ void load_crc_tables(uint32_t* lt, const uint32_t* __restrict__ tabs) {
+  const uint4* src = reinterpret_cast<const uint4*>(tabs);
+  uint4* dst = reinterpret_cast<uint4*>(lt);
+  for (int i = threadIdx.x; i < kCrcTabDw / 4; i += kBlock) dst[i] = src[i];
+  __syncthreads();
+}
+
+// crc(0, 16 bytes) with the slice tables: byte i of the chunk uses T_{15-i}.
+__device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, uint32_t w0, uint32_t w1,
+                                              uint32_t w2, uint32_t w3) {
+  const uint32_t w[4] = {w0, w1, w2, w3};
+  uint32_t r[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t* t = lt + (12 - 4 * d) * 256;  // T_{15-4d} .. T_{12-4d}
+    r[d] = xor3(t[3 * 256 + (w[d] & 0xff)], t[2 * 256 + ((w[d] >> 8) & 0xff)],
+                t[256 + ((w[d] >> 16) & 0xff)]) ^
+           t[w[d] >> 24];
+  }
+  return xor3(r[0], r[1], r[2]) ^ r[3];
+}
+
+__device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, const uint4& x) {
+  return chunk_crc(lt, x.x, x.y, x.z, x.w);
+}
+
+// Z^4096(a): the chain value followed by one tile of zero bytes.
+__device__ __forceinline__ uint32_t shift_tile(const uint32_t* lt, uint32_t a) {
+  const uint32_t* s = lt + kShiftTab;
+  return xor3(s[a & 0xff], s[256 + ((a >> 8) & 0xff)], s[512 + ((a >> 16) & 0xff)]) ^
+         s[768 + (a >> 24)];
+}
+
+// crc(0, nb bytes) one byte at a time (the lane that straddles len).
+__device__ __forceinline__ uint32_t bytes_crc(const uint32_t* lt, const uint8_t* p, int nb) {
+  uint32_t c = 0;
+  for (int i = 0; i < nb; ++i) c = (c >> 8) ^ lt[(c ^ p[i]) & 0xff];
+  return c;
+}
+
+// a * b mod P (reflected; bit 31 = x^0), as isal_hip_crc32c_mulmod.
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    p ^= (a & 0x80000000u) ? b : 0u;
+    a <<= 1;
+    b = (b >> 1) ^ ((b & 1u) ? kCrcPoly : 0u);
+  }
+  return p;
+}
+
+// ---------------------------------------------------------------------------
+// Standalone: partials of nsh shards per stripe. Item = (stripe, shard, block).
+// VEC: 16-byte aligned shards (one dwordx4 per lane and tile); otherwise byte loads.
+// ---------------------------------------------------------------------------
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void crc32c_shards(
+    const uint64_t* __restrict__ ptrs, int ptr_stride, int idx0, int nsh, int len,
+    unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, unsigned ntiles,
+    const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part, uint32_t* __restrict__ tail,
+    int nshard_total, int shard0) {
+  __shared__ uint32_t lt[kCrcTabDw];
+  load_crc_tables(lt, tabs);
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned si = w / nblk, blk = w - si * nblk;
+    const unsigned stripe = si / nsh, i = si - stripe * nsh;
+    const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + idx0 + i];
+    const size_t shard = static_cast<size_t>(stripe) * nshard_total + shard0 + i;
+    const unsigned t0 = blk * tt, t1 = t0 + tt < ntiles ? t0 + tt : ntiles;
+    uint32_t a = 0;
+    for (unsigned t = t0; t < t1; ++t) {
+      const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
+      const long long left = len - off;
+      const int nb = left >= kVec ? kVec : (left > 0 ? static_cast<int>(left) : 0);
+      uint32_t c = 0;
+      if (nb == kVec) {
+        if constexpr (VEC) {
+          c = chunk_crc(lt, load16<kBufNT>(base, off, len));
+        } else {
+          const uint8_t* p = reinterpret_cast<const uint8_t*>(base) + off;
+          uint32_t v[4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            v[d] = p[4 * d] | (p[4 * d + 1] << 8) | (p[4 * d + 2] << 16) |
+                   (static_cast<uint32_t>(p[4 * d + 3]) << 24);
+          c = chunk_crc(lt, v[0], v[1], v[2], v[3]);
+        }
+      } else if (nb > 0) {
+        c = bytes_crc(lt, reinterpret_cast<const uint8_t*>(base) + off, nb);
+      }
+      if (t < nfull)
+        a = shift_tile(lt, a) ^ c;
+      else
+        tail[shard * kBlock + threadIdx.x] = c;
+    }
+    part[(shard * nblk + blk) * kBlock + threadIdx.x] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused encode + CRC. The encode half is ec_encode_v16's (same loads, same
+// GF arithmetic, same stores); the source chunks already in registers and the
+// parity chunks about to be stored also feed the CRC chains. Source chains
+// live in LDS (lane-private words, k of them), output chains in registers.
+// ---------------------------------------------------------------------------
+struct SrcCrc {
+  const uint32_t* lt;
+  uint32_t* la;        // [k][256] source chains (LDS)
+  uint32_t* tail;      // tail row of source shard 0 of this stripe
+  bool on, full;
+  __device__ __forceinline__ void feed(int j, const uint4& x) const {
+    if (!on) return;
+    const uint32_t c = chunk_crc(lt, x);
+    if (full) {
+      uint32_t* a = la + j * kBlock + threadIdx.x;
+      *a = shift_tile(lt, *a) ^ c;
+    } else {
+      tail[static_cast<size_t>(j) * kBlock + threadIdx.x] = c;
+    }
+  }
+};
+
+template <int P, int U, int MODE>
+__device__ __forceinline__ void chunk16_crc(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
+                                            int j, long long off, const uint32_t* __restrict__ tbl,
+                                            int len, const SrcCrc& cr) {
+  uint4 x[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
+  constexpr int PAIR = P <= 4 ? 2 : 1;
+#pragma unroll
+  for (int u = 0; u + PAIR <= U; u += PAIR) {
+    if constexpr (PAIR == 2) {
+      mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
+      cr.feed(j + u, x[u]);
+      cr.feed(j + u + 1, x[u + 1]);
+    } else {
+      mac16<P>(acc, x[u], tbl + (j + u) * P * kTbl);
+      cr.feed(j + u, x[u]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (PAIR == 2 && (U & 1)) {
+    mac16<P>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl);
+    cr.feed(j + U - 1, x[U - 1]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int P, class Pol>
+__device__ __forceinline__ void accum16_crc(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
+                                            const uint32_t* __restrict__ tbl, int k, long long off,
+                                            int len, const SrcCrc& cr) {
+#pragma unroll
+  for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
+  int j = 0;
+  for (; j + Pol::U <= k; j += Pol::U) chunk16_crc<P, Pol::U, Pol::LD>(acc, src, j, off, tbl, len, cr);
+  if constexpr (Pol::U == 4) {
+    if (j + 2 <= k) {
+      chunk16_crc<P, 2, Pol::LD>(acc, src, j, off, tbl, len, cr);
+      j += 2;
+    }
+  }
+  for (; j < k; ++j) chunk16_crc<P, 1, Pol::LD>(acc, src, j, off, tbl, len, cr);
+}
+
+template <int P, int U>
+constexpr int crc_waves() {
+  constexpr int est = (4 * U + 8 * P + 56 + 7) / 8 * 8;
+  constexpr int w = 512 / est;
+  return w > 8 ? 8 : (w < 2 ? 2 : w);
+}
+
+template <int P, class Pol>
+__global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U>())) void ec_encode_crc_v16(
+    const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
+    const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned nblk, unsigned tt,
+    unsigned nfull, unsigned ntiles, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part,
+    uint32_t* __restrict__ tail, int nshard_total, int crc_src, int out_shard0) {
+  __shared__ uint32_t lt[kCrcTabDw];
+  extern __shared__ uint32_t la[];  // [k][kBlock] when crc_src
+  load_crc_tables(lt, tabs);
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned stripe = w / nblk, blk = w - stripe * nblk;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
+    const size_t shard_s = static_cast<size_t>(stripe) * nshard_total;  // source shard 0
+    const unsigned t0 = blk * tt, t1 = t0 + tt < ntiles ? t0 + tt : ntiles;
+    uint32_t ao[P];
+#pragma unroll
+    for (int l = 0; l < P; ++l) ao[l] = 0;
+    if (crc_src)
+      for (int j = 0; j < k; ++j) la[j * kBlock + threadIdx.x] = 0;
+    for (unsigned t = t0; t < t1; ++t) {
+      const bool full = t < nfull;
+      const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
+      if (off + kVec <= len) {
+        const SrcCrc cr{lt, la, tail + shard_s * kBlock, crc_src != 0, full};
+        uint32_t acc[P][4];
+        accum16_crc<P, Pol>(acc, sp + src0, tbl, k, off, len, cr);
+#pragma unroll
+        for (int l = 0; l < P; ++l) {
+          store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
+                           len);
+          const uint32_t c = chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+          if (full)
+            ao[l] = shift_tile(lt, ao[l]) ^ c;
+          else
+            tail[(shard_s + out_shard0 + l) * kBlock + threadIdx.x] = c;
+        }
+      } else if (!full) {  // lane past len in the ragged tile (len % 16 == 0)
+        if (crc_src)
+          for (int j = 0; j < k; ++j) tail[(shard_s + j) * kBlock + threadIdx.x] = 0;
+#pragma unroll
+        for (int l = 0; l < P; ++l) tail[(shard_s + out_shard0 + l) * kBlock + threadIdx.x] = 0;
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < P; ++l)
+      part[((shard_s + out_shard0 + l) * nblk + blk) * kBlock + threadIdx.x] = ao[l];
+    if (crc_src)
+      for (int j = 0; j < k; ++j)
+        part[((shard_s + j) * nblk + blk) * kBlock + threadIdx.x] = la[j * kBlock + threadIdx.x];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Combine: one workgroup per shard (grid-stride). Lane L folds its partials of
+// every block (Horner with the byte tables of x^(8*4096*tt); the last block
+// uses x^(8*4096*nfull_last)), multiplies by W[L] to move them to the shard
+// end, adds its ragged-tile chunk times Ct[L]; the XOR of all lanes plus
+// x^(8*len) * init is crc32_iscsi(shard, len, init).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void crc32c_combine(
+    const uint32_t* __restrict__ part, const uint32_t* __restrict__ tail,
+    const uint32_t* __restrict__ plan, unsigned nblk, int has_tail, unsigned init,
+    uint32_t* __restrict__ out, unsigned nsh) {
+  __shared__ uint32_t kt[2048];
+  __shared__ uint32_t red[kBlock / 64];
+  for (int i = threadIdx.x; i < 2048; i += kBlock) kt[i] = plan[i];
+  __syncthreads();
+  const uint32_t wl = plan[2048 + threadIdx.x];
+  const uint32_t cl = plan[2304 + threadIdx.x];
+  const uint32_t xlen = plan[2560];
+  for (unsigned sh = blockIdx.x; sh < nsh; sh += gridDim.x) {
+    const uint32_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + threadIdx.x;
+    uint32_t h = 0;
+    for (unsigned b = 0; b < nblk; ++b) {
+      const uint32_t* k4 = (b + 1 == nblk) ? kt + 1024 : kt;
+      h = xor3(k4[h & 0xff], k4[256 + ((h >> 8) & 0xff)], k4[512 + ((h >> 16) & 0xff)]) ^
+          k4[768 + (h >> 24)] ^ pp[static_cast<size_t>(b) * kBlock];
+    }
+    uint32_t v = crc_mulmod(h, wl);
+    if (has_tail) v ^= crc_mulmod(tail[static_cast<size_t>(sh) * kBlock + threadIdx.x], cl);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) out[sh] = red[0] ^ red[1] ^ red[2] ^ red[3] ^ crc_mulmod(init, xlen);
+    __syncthreads();
+  }
+}
+
+constexpr unsigned kMaxCrcItems = 1u << 30;
+
+unsigned crc_grid(unsigned long long nitems) {
+  return static_cast<unsigned>(nitems);
+}
+
+int enc_group_crc(int k) {
+  static const int cand[] = {12, 10, 8, 6, 5, 4};
+  for (int u : cand)
+    if (k >= u && k % u == 0) return u;
+  return 4;
+}
+
+template <int P, int U>
+void launch_fused(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
+                  int src0, int dst0, const uint32_t* tbl, int len, int k, unsigned nitems,
+                  const isal_hip_crc_geom& g, const uint32_t* tabs, uint32_t* part, uint32_t* tail,
+                  int nshard_total, int crc_src, int out_shard0) {
+  hipLaunchKernelGGL((ec_encode_crc_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), lds, s, ptrs,
+                     ptr_stride, src0, dst0, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),
+                     static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull),
+                     static_cast<unsigned>(g.ntiles), tabs, part, tail, nshard_total, crc_src,
+                     out_shard0);
+}
+
+template <int P>
+void fused_pass(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
+                int src0, int dst0, const uint32_t* tbl, int len, int k, unsigned nitems,
+                const isal_hip_crc_geom& g, const uint32_t* tabs, uint32_t* part, uint32_t* tail,
+                int nshard_total, int crc_src, int out_shard0) {
+#define FUSED_U(u)                                                                               \
+  launch_fused<P, u>(grid, lds, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, g, tabs, \
+                     part, tail, nshard_total, crc_src, out_shard0)
+  switch (enc_group_crc(k)) {
+    case 12: FUSED_U(12); break;
+    case 10: FUSED_U(10); break;
+    case 8: FUSED_U(8); break;
+    case 6: FUSED_U(6); break;
+    case 5: FUSED_U(5); break;
+    default: FUSED_U(4); break;
+  }
+#undef FUSED_U
+}
+
+}  // namespace
+
+extern "C" int isal_hip_launch_crc(const uint64_t* d_ptrs, int ptr_stride, int idx0, int nsh,
+                                   long long nstripes, int len, int vec16, int tt,
+                                   const uint32_t* d_tabs, uint32_t* d_part, uint32_t* d_tail,
+                                   int nshard_total, int shard0, void* stream) {
+  if (len <= 0 || nsh <= 0 || nstripes <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  isal_hip_crc_geom g;
+  isal_hip_crc_geometry(len, tt, &g);
+  const unsigned long long per_stripe = static_cast<unsigned long long>(nsh) * g.nblk;
+  const long long per = static_cast<long long>(kMaxCrcItems / per_stripe) > 0
+                            ? static_cast<long long>(kMaxCrcItems / per_stripe) : 1;
+  for (long long s0 = 0; s0 < nstripes; s0 += per) {
+    const long long ns = nstripes - s0 < per ? nstripes - s0 : per;
+    const unsigned nitems = static_cast<unsigned>(ns * per_stripe);
+    const uint64_t* ptrs = d_ptrs + s0 * ptr_stride;
+    uint32_t* part = d_part + static_cast<size_t>(s0) * nshard_total * g.nblk * kBlock;
+    uint32_t* tail = d_tail + static_cast<size_t>(s0) * nshard_total * kBlock;
+    if (vec16)
+      hipLaunchKernelGGL(crc32c_shards<true>, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
+                         ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
+                         static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
+                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
+    else
+      hipLaunchKernelGGL(crc32c_shards<false>, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
+                         ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
+                         static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
+                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
+    isal_hip_count_launch();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  return 0;
+}
+
+extern "C" int isal_hip_launch_encode_crc(const uint64_t* d_ptrs, int ptr_stride, int src_idx0,
+                                          int dst_idx0, const uint32_t* d_tbl, int len, int k,
+                                          int rows, long long nstripes, int tt,
+                                          const uint32_t* d_tabs, uint32_t* d_part,
+                                          uint32_t* d_tail, void* stream) {
+  if (len <= 0 || rows <= 0 || nstripes <= 0) return 0;
+  if (len % kVec || k > ISAL_HIP_CRC_MAX_FUSED_K) return static_cast<int>(hipErrorInvalidValue);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  isal_hip_crc_geom g;
+  isal_hip_crc_geometry(len, tt, &g);
+  const int nshard_total = k + rows;
+  const long long per = static_cast<long long>(kMaxCrcItems / g.nblk) > 0
+                            ? static_cast<long long>(kMaxCrcItems / g.nblk) : 1;
+  for (long long s0 = 0; s0 < nstripes; s0 += per) {
+    const long long ns = nstripes - s0 < per ? nstripes - s0 : per;
+    const unsigned nitems = static_cast<unsigned>(ns * g.nblk);
+    const uint64_t* ptrs = d_ptrs + s0 * ptr_stride;
+    uint32_t* part = d_part + static_cast<size_t>(s0) * nshard_total * g.nblk * kBlock;
+    uint32_t* tail = d_tail + static_cast<size_t>(s0) * nshard_total * kBlock;
+    for (int r0 = 0; r0 < rows; r0 += EC_MAX_ROWS_PER_PASS) {
+      const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
+      const uint32_t* tbl = d_tbl + static_cast<size_t>(kTbl) * k * r0;
+      const int crc_src = r0 == 0;
+      const size_t lds = crc_src ? static_cast<size_t>(k) * kBlock * 4 : 0;
+      switch (P) {
+#define FUSED_CASE(n)                                                                          \
+  case n:                                                                                      \
+    fused_pass<n>(crc_grid(nitems), lds, s, ptrs, ptr_stride, src_idx0, dst_idx0 + r0, tbl, len, \
+                  k, nitems, g, d_tabs, part, tail, nshard_total, crc_src, k + r0);            \
+    break;
+        FUSED_CASE(1) FUSED_CASE(2) FUSED_CASE(3) FUSED_CASE(4) FUSED_CASE(5) FUSED_CASE(6)
+        FUSED_CASE(7) FUSED_CASE(8)
+#undef FUSED_CASE
+      }
+      isal_hip_count_launch();
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+  }
+  return 0;
+}
+
+extern "C" int isal_hip_launch_crc_combine(const uint32_t* d_part, const uint32_t* d_tail,
+                                           const uint32_t* d_plan, long long nblk, int has_tail,
+                                           unsigned int init, uint32_t* out, long long nsh,
+                                           void* stream) {
+  if (nsh <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned grid = nsh < 4096 ? static_cast<unsigned>(nsh) : 4096u;
+  hipLaunchKernelGGL(crc32c_combine, dim3(grid), dim3(kBlock), 0, s, d_part, d_tail, d_plan,
+                     static_cast<unsigned>(nblk), has_tail, init, out, static_cast<unsigned>(nsh));
+  isal_hip_count_launch();
+  return static_cast<int>(hipGetLastError());
+}

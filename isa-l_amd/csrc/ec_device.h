@@ -1,0 +1,253 @@
+// ec_device.h — device-side building blocks shared by the GF(2^8) kernels
+// (ec_kernels.hip) and the fused encode+CRC kernels (crc_kernels.hip).
+// Included by exactly those translation units; everything lives in an
+// anonymous namespace (one private copy per kernel object).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "isal_hip_internal.h"
+
+namespace {
+
+constexpr int kBlock = 256;           // 4 waves of 64 lanes
+constexpr int kVec = 16;              // bytes per lane per shard
+constexpr int kTile = kBlock * kVec;  // 4 KiB column tile per workgroup step
+constexpr int kTbl = EC_TBL_DWORDS;
+
+struct Sel {
+  uint32_t s0, s1, s2;
+};
+
+// Bit-field selectors of 4 packed source bytes: bits 0-2, 3-5, 6-7 of each byte.
+__device__ __forceinline__ Sel split(uint32_t x) {
+  return {x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
+}
+
+// Wave-uniform tables of one coefficient (held in SGPRs).
+struct Coef {
+  uint32_t a0, a1, b0, b1, c;
+};
+
+__device__ __forceinline__ Coef load_coef(const uint32_t* __restrict__ t) {
+  return {t[0], t[1], t[2], t[3], t[4]};
+}
+
+// c*x for 4 packed bytes: three v_perm_b32 lookups.
+__device__ __forceinline__ uint32_t gf_mul4(const Coef& t, const Sel& s) {
+  return __builtin_amdgcn_perm(t.a1, t.a0, s.s0) ^ __builtin_amdgcn_perm(t.b1, t.b0, s.s1) ^
+         __builtin_amdgcn_perm(0u, t.c, s.s2);
+}
+
+// Shard addresses are device (global, address space 1) pointers: go through an
+// addrspace(1) pointer so hipcc emits global_load/store rather than flat_* (a
+// flat access also counts on lgkmcnt and would serialise with the SGPR table loads).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const u32x4 __attribute__((address_space(1)))* gload_t;
+typedef u32x4 __attribute__((address_space(1)))* gstore_t;
+
+// Memory access modes: 0 plain global, 1 non-temporal global (nt),
+// 2 non-temporal buffer_load/store (wave-uniform descriptor per shard, 32-bit
+// lane offset; measured +1.3 % over mode 1 on the 10-read/4-write stream,
+// profiles/r01_probe_variants_3.txt). `len` bounds the buffer descriptor.
+enum : int { kPlain = 0, kNT = 1, kBufNT = 2 };
+
+template <int MODE = kPlain>
+__device__ __forceinline__ uint4 load16(uint64_t base, long long off, int len = 0) {
+  u32x4 v;
+  if constexpr (MODE == kBufNT) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
+    const v4i r = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(off), 0, 2 /* nt */);
+    v = {static_cast<uint32_t>(r.x), static_cast<uint32_t>(r.y), static_cast<uint32_t>(r.z),
+         static_cast<uint32_t>(r.w)};
+  } else if constexpr (MODE == kNT) {
+    v = __builtin_nontemporal_load((gload_t)(base + off));
+  } else {
+    v = *(gload_t)(base + off);
+  }
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <int MODE = kPlain>
+__device__ __forceinline__ void store16(uint64_t base, long long off, uint4 v, int len = 0) {
+  if constexpr (MODE == kBufNT) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
+    const v4i w = {static_cast<int>(v.x), static_cast<int>(v.y), static_cast<int>(v.z),
+                   static_cast<int>(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, static_cast<int>(off), 0, 2 /* nt */);
+  } else {
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    if constexpr (MODE == kNT)
+      __builtin_nontemporal_store(w, (gstore_t)(base + off));
+    else
+      *(gstore_t)(base + off) = w;
+  }
+}
+
+// Tuning policy of the vector encode kernel (tools/ec_probe.hip explores others).
+//   U      sources whose loads are issued together before any arithmetic
+//   LD/ST  memory access modes of source loads / parity stores (above)
+//   ORDER  0: work item = (stripe, tile) with tile fastest; 1: stripe fastest;
+//          2: XCD-contiguous
+// Measured on MI355X (profiles/r01_probe_variants_*.txt): non-temporal loads
+// AND stores lift the 10-read/4-write stream from 5.5 to 6.1 TB/s, issuing
+// all of a stripe's source loads at once (U = k) adds ~1 %, buffer ops ~1 %;
+// the work order and shard padding do not help. The library picks U from k
+// at launch (enc_group).
+template <int UU, int LDM = kBufNT, int STM = kBufNT, int ORD = 0>
+struct EncPol {
+  static constexpr int U = UU;
+  static constexpr int LD = LDM, ST = STM;
+  static constexpr int ORDER = ORD;
+};
+template <int UU>
+using EncNT = EncPol<UU>;
+using EncDefault = EncNT<4>;
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU op (gfx950)
+}
+
+// acc[l] ^= c[l][j] * x for the P outputs of this pass; t = tables of source j.
+template <int P>
+__device__ __forceinline__ void mac16(uint32_t (&acc)[P][4], const uint4& x,
+                                      const uint32_t* __restrict__ t) {
+  const Sel s[4] = {split(x.x), split(x.y), split(x.z), split(x.w)};
+#pragma unroll
+  for (int l = 0; l < P; ++l) {
+    const Coef c = load_coef(t + l * kTbl);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t v = xor3(acc[l][d], __builtin_amdgcn_perm(c.a1, c.a0, s[d].s0),
+                              __builtin_amdgcn_perm(c.b1, c.b0, s[d].s1));
+      acc[l][d] = v ^ __builtin_amdgcn_perm(0u, c.c, s[d].s2);
+    }
+  }
+}
+
+// Two sources at once: the six lookups of a (dword, output) fold into the
+// accumulator with three 3-input XORs.
+template <int P>
+__device__ __forceinline__ void mac16x2(uint32_t (&acc)[P][4], const uint4& x, const uint4& y,
+                                        const uint32_t* __restrict__ tx,
+                                        const uint32_t* __restrict__ ty) {
+  const Sel sx[4] = {split(x.x), split(x.y), split(x.z), split(x.w)};
+  const Sel sy[4] = {split(y.x), split(y.y), split(y.z), split(y.w)};
+#pragma unroll
+  for (int l = 0; l < P; ++l) {
+    const Coef a = load_coef(tx + l * kTbl);
+    const Coef b = load_coef(ty + l * kTbl);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t v = acc[l][d];
+      v = xor3(v, __builtin_amdgcn_perm(a.a1, a.a0, sx[d].s0),
+               __builtin_amdgcn_perm(a.b1, a.b0, sx[d].s1));
+      v = xor3(v, __builtin_amdgcn_perm(0u, a.c, sx[d].s2),
+               __builtin_amdgcn_perm(b.a1, b.a0, sy[d].s0));
+      v = xor3(v, __builtin_amdgcn_perm(b.b1, b.b0, sy[d].s1),
+               __builtin_amdgcn_perm(0u, b.c, sy[d].s2));
+      acc[l][d] = v;
+    }
+  }
+}
+
+// U sources j..j+U-1: issue all U loads before any arithmetic, then fold the
+// sources in pairs; the scheduling barriers keep one pair's temporaries live
+// at a time (otherwise the scheduler hoists every lookup and spills).
+template <int P, int U, int MODE = kPlain>
+__device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
+                                        int j, long long off, const uint32_t* __restrict__ tbl,
+                                        int len) {
+  uint4 x[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
+  // Pairs share XOR3s but hold two sources' tables (2*P*5 SGPRs): only for P <= 4.
+  constexpr int PAIR = P <= 4 ? 2 : 1;
+#pragma unroll
+  for (int u = 0; u + PAIR <= U; u += PAIR) {
+    if constexpr (PAIR == 2)
+      mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
+    else
+      mac16<P>(acc, x[u], tbl + (j + u) * P * kTbl);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (PAIR == 2 && (U & 1)) {
+    mac16<P>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// First-mismatch record of the verify kernels: key = column << 8 | row. Each
+// workgroup keeps the minimum of its keys in an LDS word (ds_min_u64) and
+// writes it to its own slot at the end, so the result needs no device-scope
+// atomic and may live in pinned host memory (zero-copy small calls).
+__device__ __forceinline__ void note_mismatch(unsigned long long* bad, long long col, int row) {
+  atomicMin(bad, (static_cast<unsigned long long>(col) << 8) | static_cast<unsigned>(row));
+}
+
+// Per-byte dot product for columns [off, off+nb) of one stripe (tails,
+// unaligned shards). VERIFY: compare with the bytes at dst instead of storing.
+template <int P, bool VERIFY = false>
+__device__ __forceinline__ void dot_bytes(const uint64_t* __restrict__ sp, int src0, int dst0,
+                                          const uint32_t* __restrict__ tbl, int k, long long off,
+                                          int nb, unsigned long long* bad = nullptr, int row0 = 0,
+                                          long long col0 = 0) {
+  for (int b = 0; b < nb; ++b) {
+    uint32_t acc[P];
+#pragma unroll
+    for (int l = 0; l < P; ++l) acc[l] = 0;
+    for (int j = 0; j < k; ++j) {
+      const uint32_t x = reinterpret_cast<const uint8_t*>(sp[src0 + j])[off + b];
+      const Sel s = split(x);
+#pragma unroll
+      for (int l = 0; l < P; ++l) acc[l] ^= gf_mul4(load_coef(tbl + (j * P + l) * kTbl), s);
+    }
+#pragma unroll
+    for (int l = 0; l < P; ++l) {
+      uint8_t* d = reinterpret_cast<uint8_t*>(sp[dst0 + l]) + off + b;
+      if constexpr (VERIFY) {
+        if (static_cast<uint8_t>(acc[l]) != *d) note_mismatch(bad, col0 + off + b, row0 + l);
+      } else {
+        *d = static_cast<uint8_t>(acc[l]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Encode: coding[l] = XOR_j c[l][j] * data[j]  (ec_base.c:309-325)
+// Work item w = (stripe, 4 KiB tile), tile fastest; grid-stride over items.
+// ---------------------------------------------------------------------------
+// Waves per SIMD the register allocator must allow (VGPR budget 512/waves).
+// Live VGPRs ~ 4U (loads in flight) + 4P (accumulators) + ~32 (selectors,
+// table halves, addresses); the 512-entry file gives 512/alloc waves per SIMD.
+template <int P, int U>
+constexpr int enc_waves() {
+  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8;
+  constexpr int w = 512 / est;
+  return w > 8 ? 8 : (w < 4 ? 4 : w);
+}
+
+// acc[l] = XOR_j c[l][j] * src[j][off..off+16) for one lane.
+template <int P, class Pol>
+__device__ __forceinline__ void accum16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
+                                        const uint32_t* __restrict__ tbl, int k, long long off,
+                                        int len) {
+#pragma unroll
+  for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
+  int j = 0;
+  for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::LD>(acc, src, j, off, tbl, len);
+  // Remainder. The launcher only picks U > 4 when U divides k, so there the
+  // (cheap, correct for any k) single-source loop is dead in practice.
+  if constexpr (Pol::U == 4) {
+    if (j + 2 <= k) {
+      chunk16<P, 2, Pol::LD>(acc, src, j, off, tbl, len);
+      j += 2;
+    }
+  }
+  for (; j < k; ++j) chunk16<P, 1, Pol::LD>(acc, src, j, off, tbl, len);
+}
+
+}  // namespace

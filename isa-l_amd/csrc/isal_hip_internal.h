@@ -74,6 +74,54 @@ unsigned long long isal_hip_run(int op, int len, int k, int rows, int vec_i,
 /* Launch counter shared by the shim and the launchers. */
 void isal_hip_count_launch(void);
 
+/* ---- CRC32C of shards (crc_host.c, crc_kernels.hip) -------------------------
+ * crc32_iscsi semantics (reference crc/crc_base.c:205-219). Each workgroup
+ * covers `tt` consecutive 4 KiB tiles of one shard; lane L owns bytes
+ * [16L, 16L+16) of every tile and chains its chunks with Z^4096, leaving one
+ * partial per (shard, block, lane):
+ *   part[((shard * nblk) + blk) * 256 + L]   (shard = stripe * nshard_total + i)
+ * and, when len % 4096 != 0, the crc of its chunk of the last (ragged) tile:
+ *   tail[shard * 256 + L]
+ * crc32c_combine joins them with the constants of isal_hip_crc32c_plan. */
+#define ISAL_HIP_CRC_TILE 4096
+#define ISAL_HIP_CRC_SLICES 16
+#define ISAL_HIP_CRC_TAB_DWORDS ((ISAL_HIP_CRC_SLICES + 4) * 256)
+#define ISAL_HIP_CRC_PLAN_DWORDS (2 * 1024 + 2 * 256 + 4)
+#define ISAL_HIP_CRC_MAX_FUSED_K 64 /* fused encode keeps k source partials in LDS */
+
+typedef struct {
+        long long nfull;  /* full 4 KiB tiles */
+        int tail;         /* bytes in the ragged last tile (0: none) */
+        long long ntiles; /* nfull + (tail != 0) */
+        int tt;           /* tiles per workgroup */
+        long long nblk;   /* workgroups per shard */
+        long long nfull_last; /* full tiles in the last workgroup */
+} isal_hip_crc_geom;
+
+uint32_t isal_hip_crc32c_mulmod(uint32_t a, uint32_t b);
+uint32_t isal_hip_crc32c_xpow8n(unsigned long long n);
+void isal_hip_crc32c_tables(uint32_t *tabs);
+void isal_hip_crc_geometry(long long len, int tt, isal_hip_crc_geom *g);
+void isal_hip_crc32c_plan(long long len, int tt, uint32_t *plan);
+
+/* CRC partials of shards idx0..idx0+nsh-1 of each stripe (no encoding);
+ * shard numbering in part/tail starts at shard0 within nshard_total. */
+int isal_hip_launch_crc(const uint64_t *d_ptrs, int ptr_stride, int idx0, int nsh,
+                        long long nstripes, int len, int vec16, int tt, const uint32_t *d_tabs,
+                        uint32_t *d_part, uint32_t *d_tail, int nshard_total, int shard0,
+                        void *stream);
+/* Encode (as isal_hip_launch_encode) and leave the CRC partials of the k
+ * sources (shards 0..k-1) and the rows outputs (shards k..k+rows-1). Needs
+ * 16-byte aligned shards, len % 16 == 0 and k <= ISAL_HIP_CRC_MAX_FUSED_K. */
+int isal_hip_launch_encode_crc(const uint64_t *d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
+                               const uint32_t *d_tbl, int len, int k, int rows, long long nstripes,
+                               int tt, const uint32_t *d_tabs, uint32_t *d_part, uint32_t *d_tail,
+                               void *stream);
+/* out[sh] = crc32_iscsi of shard sh (sh < nsh) from its partials. */
+int isal_hip_launch_crc_combine(const uint32_t *d_part, const uint32_t *d_tail,
+                                const uint32_t *d_plan, long long nblk, int has_tail,
+                                unsigned int init, uint32_t *out, long long nsh, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

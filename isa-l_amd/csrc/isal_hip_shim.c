@@ -565,6 +565,10 @@ struct isal_hip_batch {
         int len, k, rows, nstripes, device, vec16;
         uint64_t *d_ptrs;
         uint32_t *d_tbl;
+        /* CRC32C state, allocated on first use: kernel tables + combine plan,
+         * and the per-lane partials (crc_kernels.hip) */
+        isal_hip_crc_geom crc;
+        uint32_t *d_crc, *d_part, *d_tail;
 };
 
 int
@@ -671,6 +675,129 @@ isal_hip_batch_destroy(isal_hip_batch *b)
                 (void) hipFree(b->d_ptrs);
         if (b->d_tbl)
                 (void) hipFree(b->d_tbl);
+        if (b->d_crc)
+                (void) hipFree(b->d_crc);
+        if (b->d_part)
+                (void) hipFree(b->d_part);
         free(b);
         return ISAL_HIP_OK;
+}
+
+/* ---- CRC32C of the batch's shards (isal_hip.h) ---------------------------- */
+
+/* Tiles per CRC workgroup: 16 (64 KiB of each shard, partials = 0.4 % of the
+ * bytes), halved while the launch would have fewer than 2048 workgroups. */
+static int
+crc_tiles(int len, int nstripes)
+{
+        const char *e = getenv("ISAL_HIP_CRC_TILES");
+        long long ntiles = ((long long) len + ISAL_HIP_CRC_TILE - 1) / ISAL_HIP_CRC_TILE;
+        int tt = e ? atoi(e) : 16;
+        if (tt < 1)
+                tt = 1;
+        if (e)
+                return tt;
+        while (tt > 1 && (long long) nstripes * ((ntiles + tt - 1) / tt) < 2048)
+                tt /= 2;
+        return tt;
+}
+
+static int
+batch_crc_setup(isal_hip_batch *b)
+{
+        uint32_t *h;
+        size_t tab = ISAL_HIP_CRC_TAB_DWORDS, plan = ISAL_HIP_CRC_PLAN_DWORDS, nsh, part, tail;
+        hipError_t e;
+        if (b->d_crc)
+                return ISAL_HIP_OK;
+        isal_hip_crc_geometry(b->len, crc_tiles(b->len, b->nstripes), &b->crc);
+        nsh = (size_t) b->nstripes * (size_t) (b->k + b->rows);
+        part = nsh * (size_t) b->crc.nblk * 256;
+        tail = nsh * 256;
+        h = (uint32_t *) malloc((tab + plan) * 4);
+        if (!h)
+                return ISAL_HIP_ENOMEM;
+        isal_hip_crc32c_tables(h);
+        isal_hip_crc32c_plan(b->len, b->crc.tt, h + tab);
+        e = hipMalloc((void **) &b->d_crc, (tab + plan) * 4);
+        if (e == hipSuccess)
+                e = hipMemcpy(b->d_crc, h, (tab + plan) * 4, hipMemcpyHostToDevice);
+        free(h);
+        if (e == hipSuccess)
+                e = hipMalloc((void **) &b->d_part, (part + tail) * 4);
+        if (e != hipSuccess) {
+                if (b->d_crc)
+                        (void) hipFree(b->d_crc);
+                b->d_crc = b->d_part = NULL;
+                return e == hipErrorOutOfMemory ? ISAL_HIP_ENOMEM : ISAL_HIP_EHIP;
+        }
+        b->d_tail = b->d_part + part;
+        return ISAL_HIP_OK;
+}
+
+static int
+batch_crc_finish(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+{
+        const long long nsh = (long long) b->nstripes * (b->k + b->rows);
+        return isal_hip_launch_crc_combine(b->d_part, b->d_tail, b->d_crc + ISAL_HIP_CRC_TAB_DWORDS,
+                                           b->crc.nblk, b->crc.tail != 0, init, (uint32_t *) crc,
+                                           nsh, stream)
+                       ? ISAL_HIP_EHIP
+                       : ISAL_HIP_OK;
+}
+
+static int
+batch_crc_empty(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+{
+        /* crc32_iscsi of 0 bytes is init_crc */
+        const size_t n = (size_t) b->nstripes * (size_t) (b->k + b->rows);
+        return hipMemsetD32Async((hipDeviceptr_t) crc, (int) init, n, (hipStream_t) stream) ==
+                               hipSuccess
+                       ? ISAL_HIP_OK
+                       : ISAL_HIP_EHIP;
+}
+
+int
+isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+{
+        int r;
+        if (!b || !crc)
+                return ISAL_HIP_EINVAL;
+        if (b->len == 0)
+                return batch_crc_empty(b, init, crc, stream);
+        if ((r = batch_crc_setup(b)) != ISAL_HIP_OK)
+                return r;
+        if (isal_hip_launch_crc(b->d_ptrs, b->k + b->rows, 0, b->k + b->rows, b->nstripes, b->len,
+                                b->vec16, b->crc.tt, b->d_crc, b->d_part, b->d_tail,
+                                b->k + b->rows, 0, stream))
+                return ISAL_HIP_EHIP;
+        return batch_crc_finish(b, init, crc, stream);
+}
+
+int
+isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+{
+        int r;
+        if (!b || !crc)
+                return ISAL_HIP_EINVAL;
+        if (b->len == 0)
+                return batch_crc_empty(b, init, crc, stream);
+        if ((r = batch_crc_setup(b)) != ISAL_HIP_OK)
+                return r;
+        if (b->vec16 && b->len % 16 == 0 && b->k <= ISAL_HIP_CRC_MAX_FUSED_K) {
+                /* one pass over the stripe: encode + CRC of all k + rows shards */
+                if (isal_hip_launch_encode_crc(b->d_ptrs, b->k + b->rows, 0, b->k, b->d_tbl, b->len,
+                                               b->k, b->rows, b->nstripes, b->crc.tt, b->d_crc,
+                                               b->d_part, b->d_tail, stream))
+                        return ISAL_HIP_EHIP;
+        } else {
+                /* unaligned shards, ragged len or very wide k: encode, then CRC */
+                if (isal_hip_batch_encode(b, stream) != ISAL_HIP_OK)
+                        return ISAL_HIP_EHIP;
+                if (isal_hip_launch_crc(b->d_ptrs, b->k + b->rows, 0, b->k + b->rows, b->nstripes,
+                                        b->len, b->vec16, b->crc.tt, b->d_crc, b->d_part,
+                                        b->d_tail, b->k + b->rows, 0, stream))
+                        return ISAL_HIP_EHIP;
+        }
+        return batch_crc_finish(b, init, crc, stream);
 }

@@ -91,6 +91,8 @@ def lib() -> ctypes.CDLL:
             "isal_hip_batch_encode": (i, [ctypes.c_void_p, ctypes.c_void_p]),
             "isal_hip_batch_update": (i, [ctypes.c_void_p, i, ctypes.c_void_p]),
             "isal_hip_batch_destroy": (i, [ctypes.c_void_p]),
+            "isal_hip_batch_encode_crc": (i, [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]),
+            "isal_hip_batch_crc": (i, [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]),
             "isal_hip_pipe_create": (i, [ctypes.POINTER(ctypes.c_void_p), i, i, i, _u8p, i, i]),
             "isal_hip_pipe_submit": (i, [ctypes.c_void_p, _u8pp, _u8pp]),
             "isal_hip_pipe_flush": (i, [ctypes.c_void_p]),
@@ -271,6 +273,22 @@ class Batch:
         rc = lib().isal_hip_batch_update(self._h, vec_i, ctypes.c_void_p(stream))
         if rc != 0:
             raise RuntimeError(f"isal_hip_batch_update failed ({rc})")
+
+    def encode_crc(self, init: int, crc, stream: int = 0) -> None:
+        """encode() plus crc32_iscsi(shard, len, init) of every source and parity
+        shard into the DEVICE buffer crc (nstripes*(k+rows) uint32, stripe-major,
+        sources then parity)."""
+        rc = lib().isal_hip_batch_encode_crc(self._h, init & 0xFFFFFFFF, ctypes.c_void_p(addr(crc)),
+                                             ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_encode_crc failed ({rc})")
+
+    def crc(self, init: int, crc, stream: int = 0) -> None:
+        """crc32_iscsi of every shard (no encoding), layout as encode_crc()."""
+        rc = lib().isal_hip_batch_crc(self._h, init & 0xFFFFFFFF, ctypes.c_void_p(addr(crc)),
+                                      ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_crc failed ({rc})")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -95,3 +95,66 @@ gfni_port_ec_encode_data(int len, int k, int rows, const unsigned char *tbls,
                 dot_group(len, k, n, mat, src, dst + r0);
         }
 }
+
+/* ---- crc32_iscsi with the SSE4.2 crc32 instruction (baseline only) --------
+ * The reference's fast CRC32C (crc/crc32_iscsi_01.asm, crc32_iscsi_by16_10.asm)
+ * is NASM too. Restated here the way crc32_iscsi_01 works: three independent
+ * crc32q streams over the buffer's thirds (the instruction's 3-cycle latency
+ * hides behind the other two streams), joined by shifting the first two
+ * streams past the bytes that follow them (the reference uses PCLMUL for that
+ * join; a bitwise multiply mod P is equivalent and costs nothing at 1 MiB). */
+static uint32_t
+crc_mulmod(uint32_t a, uint32_t b)
+{
+        uint32_t p = 0;
+        int i;
+        for (i = 0; i < 32; i++) {
+                if (a & 0x80000000u)
+                        p ^= b;
+                a <<= 1;
+                b = (b & 1) ? (b >> 1) ^ 0x82F63B78u : b >> 1;
+        }
+        return p;
+}
+
+static uint32_t
+crc_shift(uint32_t crc, uint64_t nbytes) /* crc followed by nbytes zero bytes */
+{
+        uint32_t sq = 0x00800000u; /* x^8 */
+        while (nbytes) {
+                if (nbytes & 1)
+                        crc = crc_mulmod(crc, sq);
+                sq = crc_mulmod(sq, sq);
+                nbytes >>= 1;
+        }
+        return crc;
+}
+
+__attribute__((target("sse4.2"))) unsigned int
+gfni_port_crc32_iscsi(const unsigned char *buf, long long len, unsigned int init)
+{
+        uint64_t c0 = init, c1 = 0, c2 = 0, w0, w1, w2;
+        long long third = (len / 24) * 8, i;
+        const unsigned char *p1 = buf + third, *p2 = buf + 2 * third, *end = buf + len;
+        for (i = 0; i < third; i += 8) {
+                memcpy(&w0, buf + i, 8);
+                memcpy(&w1, p1 + i, 8);
+                memcpy(&w2, p2 + i, 8);
+                c0 = _mm_crc32_u64(c0, w0);
+                c1 = _mm_crc32_u64(c1, w1);
+                c2 = _mm_crc32_u64(c2, w2);
+        }
+        {
+                const unsigned char *q = p2 + third;
+                uint32_t c = (uint32_t) c2;
+                for (; q + 8 <= end; q += 8) {
+                        memcpy(&w2, q, 8);
+                        c = (uint32_t) _mm_crc32_u64(c, w2);
+                }
+                for (; q < end; q++)
+                        c = _mm_crc32_u8(c, *q);
+                /* join: stream 0 is followed by 2 thirds + the rest, stream 1 by 1 third + rest */
+                return crc_shift((uint32_t) c0, (uint64_t) (len - third)) ^
+                       crc_shift((uint32_t) c1, (uint64_t) (len - 2 * third)) ^ c;
+        }
+}

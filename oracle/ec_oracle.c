@@ -345,3 +345,33 @@ oracle_pq_check(int vects, int len, unsigned char **a)
         }
         return 0;
 }
+
+/* ---- CRC32C (reference crc/crc_base.c) ------------------------------------ */
+
+/* crc_base.c:205-219 (crc32_iscsi_base): table-driven reflected CRC32C, the
+ * register starts at crc_init, no final inversion. The reference's literal
+ * table crc32_table_iscsi_refl (crc_base.c:58-...) is the byte table of the
+ * reflected Castagnoli polynomial 0x82F63B78 (crc/crc_ref.h:47-61 computes the
+ * same CRC bit by bit); it is regenerated here from the polynomial. */
+static unsigned int crc32c_tab[256];
+static int crc32c_ready;
+
+unsigned int
+oracle_crc32_iscsi(const unsigned char *buf, long long len, unsigned int init)
+{
+        unsigned int crc = init;
+        long long i;
+        if (!crc32c_ready) {
+                int b, k;
+                for (b = 0; b < 256; b++) {
+                        unsigned int c = (unsigned int) b;
+                        for (k = 0; k < 8; k++)
+                                c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+                        crc32c_tab[b] = c;
+                }
+                crc32c_ready = 1;
+        }
+        for (i = 0; i < len; i++)
+                crc = (crc >> 8) ^ crc32c_tab[(crc ^ buf[i]) & 0xff];
+        return crc;
+}

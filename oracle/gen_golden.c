@@ -36,6 +36,8 @@ int xor_gen(int vects, int len, void **array);
 int xor_check(int vects, int len, void **array);
 int pq_gen(int vects, int len, void **array);
 int pq_check(int vects, int len, void **array);
+/* Reference crc ABI (reference include/crc.h:137-151; crc/crc_base.c). */
+unsigned int crc32_iscsi_base(unsigned char *buffer, int len, unsigned int crc_init);
 
 static FILE *out;
 static int first_item;
@@ -529,6 +531,42 @@ main(int argc, char **argv)
                                 }
                         }
                 }
+        }
+        fprintf(out, "]");
+
+        /* CRC32C (reference crc_base.c crc32_iscsi_base): the fused fragment
+         * checksum of the engine must equal it. The shapes follow
+         * crc32_funcs_test.c (zero buffer, 0x8a buffer, random sizes) plus
+         * the tile boundaries of the GPU kernels (4 KiB tiles, 16 B lanes). */
+        fprintf(out, ",\n  \"crc32_iscsi\": [");
+        first_item = 1;
+        {
+                static const int lens[] = { 0, 1, 3, 15, 16, 17, 255, 256, 1000, 4080, 4095, 4096,
+                                            4097, 4112, 8192, 65536, 65536 + 16, 65536 * 3 + 4000,
+                                            1 << 20 };
+                static const unsigned int inits[] = { 0u, 0xffffffffu, 0x12345678u };
+                int li, ii;
+                for (li = 0; li < (int) (sizeof(lens) / sizeof(lens[0])); li++)
+                        for (ii = 0; ii < 3; ii++) {
+                                const int len = lens[li];
+                                const unsigned long long seed = 1000 + li * 7 + ii;
+                                unsigned char *b = malloc((size_t) len + 1);
+                                int kind = (li + ii) % 5 == 0 ? 1 : ((li + ii) % 7 == 0 ? 2 : 0);
+                                if (kind == 1)
+                                        memset(b, 0, len);
+                                else if (kind == 2)
+                                        memset(b, 0x8a, len);
+                                else
+                                        fill_bytes(b, len, seed);
+                                item_sep();
+                                fprintf(out,
+                                        "{\"len\": %d, \"init\": %u, \"fill\": \"%s\", "
+                                        "\"seed\": %llu, \"crc\": %u}",
+                                        len, inits[ii],
+                                        kind == 1 ? "zero" : (kind == 2 ? "8a" : "splitmix"), seed,
+                                        crc32_iscsi_base(b, len, inits[ii]));
+                                free(b);
+                        }
         }
         fprintf(out, "]\n}\n");
         fclose(out);

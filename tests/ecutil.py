@@ -86,6 +86,8 @@ class Oracle:
         L.oracle_gf_vect_mul.restype = ctypes.c_int
         L.oracle_fnv1a32.restype = ctypes.c_uint
         L.oracle_fnv1a32.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+        L.oracle_crc32_iscsi.restype = ctypes.c_uint
+        L.oracle_crc32_iscsi.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_uint]
         self.L = L
 
     def gf_mul(self, a, b):
@@ -142,6 +144,11 @@ class Oracle:
         f.restype = ctypes.c_int
         return int(f(vects, length, _pp(arrs)))
 
+    def crc32_iscsi(self, a: np.ndarray, init: int) -> int:
+        """crc_base.c crc32_iscsi_base(buf, len, init) (oracle restatement)."""
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        return int(self.L.oracle_crc32_iscsi(ctypes.c_void_p(a.ctypes.data), a.size, init & 0xFFFFFFFF))
+
     def fnv(self, a: np.ndarray) -> int:
         return int(self.L.oracle_fnv1a32(ctypes.c_void_p(a.ctypes.data), a.size))
 
@@ -167,6 +174,16 @@ def coeffs(gen: str, k: int, rows: int, seed: int, o: Oracle | None = None) -> n
     if gen == "cauchy":
         return o.gf_gen_cauchy1_matrix(k + rows, k)[k * k:].copy()
     return fill_bytes(k * rows, seed ^ 0xC0EFF1C1E47)
+
+
+def crc_fixture_bytes(entry: dict) -> np.ndarray:
+    """Input buffer of one tests/golden crc32_iscsi entry (gen_golden.c)."""
+    n = entry["len"]
+    if entry["fill"] == "zero":
+        return np.zeros(n, np.uint8)
+    if entry["fill"] == "8a":
+        return np.full(n, 0x8A, np.uint8)
+    return fill_bytes(n, entry["seed"])
 
 
 def decode_matrix(a: np.ndarray, k: int, errs, o: Oracle | None = None):

@@ -238,3 +238,34 @@ def test_oracle_raid(oracle):
         assert oracle.fnv(bx[v - 1]) == case["xor_fnv"]
         if v >= 4:
             assert oracle.fnv(bp[v - 2]) == case["p_fnv"] and oracle.fnv(bp[v - 1]) == case["q_fnv"]
+
+
+def test_oracle_crc32_iscsi(oracle):
+    """oracle restatement of crc_base.c crc32_iscsi_base == the reference's outputs
+    (tests/golden crc32_iscsi section), plus the standard CRC32C check value."""
+    from ecutil import crc_fixture_bytes
+
+    cases = golden()["crc32_iscsi"]
+    assert len(cases) >= 50
+    for case in cases:
+        assert oracle.crc32_iscsi(crc_fixture_bytes(case), case["init"]) == case["crc"], case
+    # CRC-32C check value (RFC 3720 convention: init ~0, final ~): 0xE3069283
+    msg = np.frombuffer(b"123456789", np.uint8)
+    assert oracle.crc32_iscsi(msg, 0xFFFFFFFF) ^ 0xFFFFFFFF == 0xE3069283
+
+
+def test_simd_port_crc32_iscsi_matches_oracle(oracle):
+    """The SSE4.2 crc32 baseline (oracle/ec_gfni_port.c) == oracle crc32_iscsi."""
+    import ctypes
+    import os
+
+    path = os.path.join(ecutil.ORACLE_DIR, "libgfni_port.so")
+    if not os.path.exists(path):
+        pytest.skip("libgfni_port.so not built")
+    G = ctypes.CDLL(path)
+    G.gfni_port_crc32_iscsi.restype = ctypes.c_uint
+    G.gfni_port_crc32_iscsi.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_uint]
+    for n in (0, 1, 7, 8, 23, 24, 25, 4096, 65536 + 5):
+        a = fill_bytes(n, n + 11)
+        init = (n * 2654435761) & 0xFFFFFFFF
+        assert G.gfni_port_crc32_iscsi(a.ctypes.data, n, init) == oracle.crc32_iscsi(a, init), n

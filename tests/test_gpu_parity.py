@@ -308,6 +308,124 @@ def test_config_c2_c3_full_size(engine, oracle, gpu):
     dec.close()
 
 
+# --------------------------------------------------------------------------
+# fused fragment checksums (CRC32C = reference crc32_iscsi) — SURVEY §8(f)
+# --------------------------------------------------------------------------
+
+def test_crc_golden_fixtures(engine, oracle, gpu):
+    """isal_hip_batch_crc of one shard == the reference's crc32_iscsi_base outputs
+    (tests/golden crc32_iscsi: zero / 0x8a / random buffers, lengths across the
+    16-byte lane and 4 KiB tile boundaries, three init values)."""
+    import torch
+
+    from ecutil import crc_fixture_bytes
+
+    tbls = engine.ec_init_tables(1, 1, np.array([1], np.uint8))
+    out = torch.zeros(2, dtype=torch.int32, device=gpu)
+    for case in golden()["crc32_iscsi"]:
+        n = case["len"]
+        src = _dev(torch, crc_fixture_bytes(case), gpu) if n else torch.zeros(16, dtype=torch.uint8, device=gpu)
+        dst = torch.zeros(max(n, 16), dtype=torch.uint8, device=gpu)
+        b = engine.Batch(n, 1, 1, tbls, 1, [int(src.data_ptr())], [int(dst.data_ptr())])
+        b.crc(case["init"], out, 0)
+        torch.cuda.synchronize()
+        assert int(out[0].item()) & 0xFFFFFFFF == case["crc"], case
+        b.encode_crc(case["init"], out, 0)  # parity = 1 * src: both CRCs equal
+        torch.cuda.synchronize()
+        got = [int(v) & 0xFFFFFFFF for v in out.tolist()]
+        assert got == [case["crc"], case["crc"]], case
+        b.close()
+
+
+CRC_SHAPES = [
+    # k, rows, len, nstripes, byte offset of every shard (0: 16-B aligned)
+    (10, 4, 65536, 9, 0),             # C2 shape, fused path, tt halving
+    (10, 4, 4096 * 37 + 2048, 5, 0),  # ragged last tile, 16-B multiple
+    (4, 2, 65536 + 4000, 3, 0),       # fused, ragged tile
+    (6, 3, 1000, 4, 0),               # single partial tile
+    (3, 2, 4096 * 3 + 13, 3, 0),      # len % 16 != 0 -> encode + CRC pass
+    (5, 5, 20000, 2, 1),              # unaligned shards -> byte-load CRC kernel
+    (4, 10, 4096 * 5, 2, 0),          # rows > 8: two fused passes
+    (70, 3, 4096 * 2 + 32, 2, 0),     # k > 64: encode + CRC pass
+    (1, 1, 16, 3, 0),
+]
+
+
+@pytest.mark.parametrize("k,rows,n,ns,skew", CRC_SHAPES)
+def test_encode_crc_vs_oracle(engine, oracle, gpu, k, rows, n, ns, skew):
+    """Fused encode + CRC: parity == oracle encode, every shard's CRC == oracle
+    crc32_iscsi; the checksum-only pass agrees."""
+    import torch
+
+    rng = np.random.default_rng(k * 1000 + n)
+    a = oracle.gf_gen_rs_matrix(k + rows, k) if k + rows <= 32 else rng.integers(0, 256, (k + rows) * k, dtype=np.uint8)
+    coef = a[k * k:].copy()
+    tbls = engine.ec_init_tables(k, rows, coef)
+    stride = n + 64
+    pool = torch.zeros(ns * (k + rows) * stride + 64, dtype=torch.uint8, device=gpu)
+    h_data = [[fill_bytes(n, 7 * s + j + n) for j in range(k)] for s in range(ns)]
+
+    def at(s, i):
+        return (s * (k + rows) + i) * stride + skew
+
+    for s in range(ns):
+        for j in range(k):
+            pool[at(s, j):at(s, j) + n] = _dev(torch, h_data[s][j], gpu)
+    base = int(pool.data_ptr())
+    dptr = [base + at(s, j) for s in range(ns) for j in range(k)]
+    cptr = [base + at(s, k + l) for s in range(ns) for l in range(rows)]
+    init = 0x9E3779B9 ^ n
+    crc = torch.zeros(ns * (k + rows), dtype=torch.int32, device=gpu)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.encode_crc(init, crc, 0)
+    torch.cuda.synchronize()
+    h_pool, got = _host(pool), [int(v) & 0xFFFFFFFF for v in crc.tolist()]
+    for s in range(ns):
+        want = oracle.encode(coef, k, rows, h_data[s])
+        shards = h_data[s] + want
+        for l in range(rows):
+            assert np.array_equal(h_pool[at(s, k + l):at(s, k + l) + n], want[l]), (s, l)
+        for i, buf in enumerate(shards):
+            assert got[s * (k + rows) + i] == oracle.crc32_iscsi(buf, init), (s, i)
+    crc2 = torch.zeros_like(crc)
+    b.crc(init, crc2, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(crc, crc2)
+    b.close()
+
+
+def test_encode_crc_c2_full_size(engine, oracle, gpu):
+    """C2 at full size through the fused path: parity identical to the plain
+    encode kernel's, CRCs == oracle on sampled stripes and == the standalone
+    checksum pass on all 14336 shards."""
+    import torch
+
+    k, p, n, ns = 10, 4, 1 << 20, 1024
+    a = engine.gf_gen_rs_matrix(k + p, k)
+    tbls = engine.ec_init_tables(k, p, a[k * k:])
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, p, n, 77)
+    b = engine.Batch(n, k, p, tbls, ns, dptr, cptr)
+    b.encode(0)
+    torch.cuda.synchronize()
+    ref = coding.clone()
+    coding.zero_()
+    crc = torch.zeros(ns * (k + p), dtype=torch.int32, device=gpu)
+    b.encode_crc(0xFFFFFFFF, crc, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(coding, ref)
+    del ref
+    got = crc.view(ns, k + p)
+    for s in (0, 1, 333, 1023):
+        for i in range(k + p):
+            buf = _host(data[s, i]) if i < k else _host(coding[s, i - k])
+            assert int(got[s, i].item()) & 0xFFFFFFFF == oracle.crc32_iscsi(buf, 0xFFFFFFFF), (s, i)
+    crc2 = torch.zeros_like(crc)
+    b.crc(0xFFFFFFFF, crc2, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(crc, crc2)
+    b.close()
+
+
 def test_config_c4_streaming_update_k20_p6(engine, oracle, gpu):
     """C4: k=20 p=6, 4 MiB shards, 20 ec_encode_data_update calls into pre-zeroed
     parity == ec_encode_data, and == oracle on a sampled window."""
