@@ -1,0 +1,78 @@
+#!/bin/bash
+# One GPU-box session: parity tests, benches, rocprofv3 kernel stats.
+# Usage (from the repo root, via gpurun): bash tools/gpu_session.sh TAG [steps...]
+#   steps: tests bench crc prof pmc decode update e2e probe
+# Every GPU step runs under its own timeout and the chain stops at the first
+# failure; outputs land in gpurun_out/TAG/.
+set -o pipefail
+TAG=${1:-run}
+shift
+STEPS=${*:-tests bench}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+export PYTHONUNBUFFERED=1
+
+run() {  # name seconds cmd...
+        local name=$1 secs=$2
+        shift 2
+        echo "[$(date +%T)] $name: $*"
+        timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+        local rc=$?
+        tail -3 "$OUT/$name.log"
+        if [ $rc -ne 0 ]; then
+                echo "[$(date +%T)] $name FAILED rc=$rc"
+                tail -40 "$OUT/$name.log"
+                exit $rc
+        fi
+}
+
+for s in $STEPS; do
+        case $s in
+        tests)
+                run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+                grep -E "PASSED|FAILED|SKIPPED|ERROR|passed|failed" "$OUT/pytest_gpu.log" > "$OUT/pytest_gpu_summary.txt" || true
+                ;;
+        bench)
+                run bench_c2 300 python bench.py
+                cp "$OUT/bench_c2.log" "$OUT/bench_c2.json"
+                ;;
+        crc)
+                run bench_encode_crc 300 python bench.py --workload encode-crc
+                run bench_crc 300 python bench.py --workload crc --cpu-seconds 5
+                ;;
+        decode)
+                run bench_decode 300 python bench.py --workload decode --no-cpu-baseline
+                ;;
+        update)
+                run bench_update 300 python bench.py --workload update --k 20 --p 6 --len 4194304 --stripes 64 --no-cpu-baseline
+                ;;
+        e2e)
+                run bench_e2e_update 300 python bench.py --workload e2e-update --k 20 --p 6 --len 4194304 --steps 40 --warmup 4
+                run bench_e2e_encode 300 python bench.py --workload e2e-encode --steps 200 --warmup 10
+                ;;
+        prof)
+                run rocprof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c2" -o c2 -- python3 bench.py --no-cpu-baseline
+                cp "$OUT/rocprof_c2.log" "$OUT/bench_c2_under_rocprof.log"
+                run rocprof_crc 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_crc" -o crc -- python3 bench.py --workload encode-crc --no-cpu-baseline
+                run rocprof_crconly 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_crconly" -o crconly -- python3 bench.py --workload crc --no-cpu-baseline
+                ;;
+        pmc)
+                for wl in encode encode-crc crc; do
+                        run pmc_fetch_$wl 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$wl" -o f -- python3 bench.py --workload $wl --no-cpu-baseline --steps 3 --warmup 1
+                        run pmc_write_$wl 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$wl" -o w -- python3 bench.py --workload $wl --no-cpu-baseline --steps 3 --warmup 1
+                done
+                python3 tools/pmc_csv.py "$OUT/pmc_c2_encode.csv" "workload=encode k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encode" "$OUT/pmc_write_encode" ec_encode_v16
+                python3 tools/pmc_csv.py "$OUT/pmc_c2_encode_crc.csv" "workload=encode-crc k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode-crc --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encode-crc" "$OUT/pmc_write_encode-crc" ec_encode_crc_v16
+                python3 tools/pmc_csv.py "$OUT/pmc_c2_crc.csv" "workload=crc k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload crc --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_crc" "$OUT/pmc_write_crc" crc32c_shards
+                ;;
+        probe)
+                run probe 300 isa-l_amd/build/ec_probe
+                ;;
+        *)
+                echo "unknown step $s"
+                exit 2
+                ;;
+        esac
+done
+echo "[$(date +%T)] session $TAG done"
