@@ -82,22 +82,52 @@ mul_tables(uint32_t k, uint32_t *out)
                         out[q * 256 + v] = isal_hip_crc32c_mulmod((uint32_t) v << (8 * q), k);
 }
 
-/* Kernel lookup tables (ISAL_HIP_CRC_TAB_DWORDS): slice tables T_j, j < 16
- * (T_j[b] = crc of byte b followed by j zero bytes), then the four byte tables
- * of Z^4096 (one 4 KiB tile of zeros). */
+/* First bit and width of field f of a dword (ISAL_HIP_CRC_FIELDS fields). */
+static int
+field_lo(int f)
+{
+        return 5 * f;
+}
+
+static int
+field_bits(int f)
+{
+        return f < ISAL_HIP_CRC_FIELDS - 1 ? 5 : 32 - 5 * (ISAL_HIP_CRC_FIELDS - 1);
+}
+
+/* Kernel lookup tables (ISAL_HIP_CRC_TAB_DWORDS, layout in
+ * isal_hip_internal.h). The field tables follow from linearity: a field's
+ * contribution is the XOR of the contributions of its set bits, and bit j of
+ * byte i of a 16-byte chunk contributes slice_{15-i}[1 << j], where slice_s[b]
+ * is the crc of byte b followed by s zero bytes. */
 void
 isal_hip_crc32c_tables(uint32_t *tabs)
 {
-        int j, b;
+        uint32_t slice[ISAL_HIP_CRC_SLICES][256];
+        const uint32_t zk = isal_hip_crc32c_xpow8n(ISAL_HIP_CRC_TILE);
+        int s, b, d, f, v, j;
         pthread_once(&once, init);
         for (b = 0; b < 256; b++)
-                tabs[b] = t0[b];
-        for (j = 1; j < ISAL_HIP_CRC_SLICES; j++)
+                slice[0][b] = tabs[b] = t0[b];
+        for (s = 1; s < ISAL_HIP_CRC_SLICES; s++)
                 for (b = 0; b < 256; b++) {
-                        const uint32_t c = tabs[(j - 1) * 256 + b];
-                        tabs[j * 256 + b] = (c >> 8) ^ t0[c & 0xff];
+                        const uint32_t c = slice[s - 1][b];
+                        slice[s][b] = (c >> 8) ^ t0[c & 0xff];
                 }
-        mul_tables(isal_hip_crc32c_xpow8n(ISAL_HIP_CRC_TILE), tabs + ISAL_HIP_CRC_SLICES * 256);
+        for (f = 0; f < ISAL_HIP_CRC_FIELDS; f++)
+                for (v = 0; v < 32; v++) {
+                        /* value v in field f, restricted to the field's width */
+                        const uint32_t word = (uint32_t) (v & ((1 << field_bits(f)) - 1))
+                                              << field_lo(f);
+                        for (d = 0; d < 4; d++) {
+                                uint32_t c = 0;
+                                for (j = 0; j < 32; j++)
+                                        if (word >> j & 1)
+                                                c ^= slice[15 - (4 * d + j / 8)][1u << (j % 8)];
+                                tabs[ISAL_HIP_CRC_CHUNK_TAB + (d * ISAL_HIP_CRC_FIELDS + f) * 32 + v] = c;
+                        }
+                        tabs[ISAL_HIP_CRC_SHIFT_TAB + f * 32 + v] = isal_hip_crc32c_mulmod(word, zk);
+                }
 }
 
 /* Geometry of the per-lane partials for shards of `len` bytes, `tt` tiles per

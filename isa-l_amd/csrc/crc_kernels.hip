@@ -19,6 +19,8 @@
 //    block XOR-reduction, then adds Z^len(init_crc).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "ec_device.h"
 
@@ -26,7 +28,7 @@ namespace {
 
 constexpr uint32_t kCrcPoly = 0x82F63B78u;
 constexpr int kCrcTabDw = ISAL_HIP_CRC_TAB_DWORDS;
-constexpr int kShiftTab = ISAL_HIP_CRC_SLICES * 256;  // Z^4096 byte tables follow the slices
+
 static_assert(ISAL_HIP_CRC_TILE == kTile, "CRC tile = encode tile");
 
 __device__ __forceinline__ void load_crc_tables(uint32_t* lt, const uint32_t* __restrict__ tabs) {
@@ -36,19 +38,48 @@ __device__ __forceinline__ void load_crc_tables(uint32_t* lt, const uint32_t* __
   __syncthreads();
 }
 
-// crc(0, 16 bytes) with the slice tables: byte i of the chunk uses T_{15-i}.
+// Byte offsets (entry index * 4) of the 7 fields of w, bits [0,5) [5,10)
+// [10,15) [15,20) [20,25) [25,30) [30,32): 11 VALU ops for 7 lookups. Shifting
+// w left by 2 puts every field at its entry's byte offset; masking the even
+// and the odd fields into separate words leaves two zero bits below each
+// field, so one bit-field extract yields the offset.
+// One v_bfe_u32. (Through the builtin, LLVM sees that the two low bits are
+// zero, narrows the mask to a non-contiguous one and emits shift + and.)
+template <int OFF, int WIDTH>
+__device__ __forceinline__ uint32_t bfe(uint32_t x) {
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "n"(OFF), "n"(WIDTH));
+  return r;
+}
+
+__device__ __forceinline__ void field_offsets(uint32_t w, uint32_t (&o)[ISAL_HIP_CRC_FIELDS]) {
+  const uint32_t s = w << 2;
+  const uint32_t ev = s & 0x07C1F07Cu;  // fields 0, 2, 4 at [2,7) [12,17) [22,27)
+  const uint32_t od = s & 0xF83E0F80u;  // fields 1, 3, 5 at [7,12) [17,22) [27,32)
+  o[0] = ev & 0x7Cu;
+  o[1] = bfe<5, 7>(od);
+  o[2] = bfe<10, 7>(ev);
+  o[3] = bfe<15, 7>(od);
+  o[4] = bfe<20, 7>(ev);
+  o[5] = bfe<25, 7>(od);
+  o[6] = (w >> 28) & 0xCu;
+}
+
+// XOR of the 7 field lookups of w in the 7 consecutive 32-entry tables at t.
+__device__ __forceinline__ uint32_t lookup7(const uint32_t* t, uint32_t w) {
+  uint32_t o[ISAL_HIP_CRC_FIELDS];
+  field_offsets(w, o);
+  const char* b = reinterpret_cast<const char*>(t);
+  auto at = [&](int f) { return *reinterpret_cast<const uint32_t*>(b + f * 128 + o[f]); };
+  return xor3(xor3(at(0), at(1), at(2)), xor3(at(3), at(4), at(5)), at(6));
+}
+
+// crc(0, 16 bytes): 28 conflict-free lookups.
 __device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, uint32_t w0, uint32_t w1,
                                               uint32_t w2, uint32_t w3) {
-  const uint32_t w[4] = {w0, w1, w2, w3};
-  uint32_t r[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t* t = lt + (12 - 4 * d) * 256;  // T_{15-4d} .. T_{12-4d}
-    r[d] = xor3(t[3 * 256 + (w[d] & 0xff)], t[2 * 256 + ((w[d] >> 8) & 0xff)],
-                t[256 + ((w[d] >> 16) & 0xff)]) ^
-           t[w[d] >> 24];
-  }
-  return xor3(r[0], r[1], r[2]) ^ r[3];
+  const uint32_t* t = lt + ISAL_HIP_CRC_CHUNK_TAB;
+  constexpr int D = ISAL_HIP_CRC_FIELDS * 32;  // tables per dword of the chunk
+  return xor3(lookup7(t, w0), lookup7(t + D, w1), lookup7(t + 2 * D, w2)) ^ lookup7(t + 3 * D, w3);
 }
 
 __device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, const uint4& x) {
@@ -57,9 +88,7 @@ __device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, const uint4& x
 
 // Z^4096(a): the chain value followed by one tile of zero bytes.
 __device__ __forceinline__ uint32_t shift_tile(const uint32_t* lt, uint32_t a) {
-  const uint32_t* s = lt + kShiftTab;
-  return xor3(s[a & 0xff], s[256 + ((a >> 8) & 0xff)], s[512 + ((a >> 16) & 0xff)]) ^
-         s[768 + (a >> 24)];
+  return lookup7(lt + ISAL_HIP_CRC_SHIFT_TAB, a);
 }
 
 // crc(0, nb bytes) one byte at a time (the lane that straddles len).
@@ -85,6 +114,10 @@ __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
 // Standalone: partials of nsh shards per stripe. Item = (stripe, shard, block).
 // VEC: 16-byte aligned shards (one dwordx4 per lane and tile); otherwise byte loads.
 // ---------------------------------------------------------------------------
+// Full tiles are read kCrcBatch at a time (all loads issued before any lookup):
+// one 16-byte load in flight per lane leaves the kernel latency-bound.
+constexpr unsigned kCrcBatch = 8;
+
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void crc32c_shards(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int idx0, int nsh, int len,
@@ -100,7 +133,31 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards(
     const size_t shard = static_cast<size_t>(stripe) * nshard_total + shard0 + i;
     const unsigned t0 = blk * tt, t1 = t0 + tt < ntiles ? t0 + tt : ntiles;
     uint32_t a = 0;
-    for (unsigned t = t0; t < t1; ++t) {
+    unsigned t = t0;
+    if constexpr (VEC) {
+      const unsigned tf = t1 < nfull ? t1 : nfull;  // full tiles of this block
+      // double-buffered: batch b+1 is in flight while batch b is checksummed
+      uint4 xn[kCrcBatch];
+      const long long lane = threadIdx.x * kVec;
+      if (t + kCrcBatch <= tf) {
+#pragma unroll
+        for (unsigned g = 0; g < kCrcBatch; ++g)
+          xn[g] = load16<kBufNT>(base, static_cast<long long>(t + g) * kTile + lane, len);
+      }
+      for (; t + kCrcBatch <= tf; t += kCrcBatch) {
+        uint4 x[kCrcBatch];
+#pragma unroll
+        for (unsigned g = 0; g < kCrcBatch; ++g) x[g] = xn[g];
+        if (t + 2 * kCrcBatch <= tf) {
+#pragma unroll
+          for (unsigned g = 0; g < kCrcBatch; ++g)
+            xn[g] = load16<kBufNT>(base, static_cast<long long>(t + kCrcBatch + g) * kTile + lane, len);
+        }
+#pragma unroll
+        for (unsigned g = 0; g < kCrcBatch; ++g) a = shift_tile(lt, a) ^ chunk_crc(lt, x[g]);
+      }
+    }
+    for (; t < t1; ++t) {
       const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
       const long long left = len - off;
       const int nb = left >= kVec ? kVec : (left > 0 ? static_cast<int>(left) : 0);
@@ -132,126 +189,213 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards(
 // ---------------------------------------------------------------------------
 // Fused encode + CRC. The encode half is ec_encode_v16's (same loads, same
 // GF arithmetic, same stores); the source chunks already in registers and the
-// parity chunks about to be stored also feed the CRC chains. Source chains
-// live in LDS (lane-private words, k of them), output chains in registers.
+// parity chunks about to be stored also feed the CRC chains. Output chains
+// live in registers; source chains too when the stripe's k sources form one
+// load group (REG: k == U, e.g. C2's k = 10), else in LDS (lane-private words).
+// Full tiles run a branch-free loop; the ragged last tile (len % 4096 != 0)
+// runs once, after it, with the chunk CRCs going to tail[].
 // ---------------------------------------------------------------------------
-struct SrcCrc {
+enum : int {
+  kFeedReg = 0,   // full tile, source chain in registers
+  kFeedLds = 1,   // full tile, source chain in LDS
+  kFeedTail = 2,  // ragged tile: the chunk's crc goes to tail[]
+  kFeedNone = 3,  // no source checksums (second pass of rows > 8)
+};
+
+template <int FEED>
+struct SrcFeed {
   const uint32_t* lt;
-  uint32_t* la;        // [k][256] source chains (LDS)
-  uint32_t* tail;      // tail row of source shard 0 of this stripe
-  bool on, full;
-  __device__ __forceinline__ void feed(int j, const uint4& x) const {
-    if (!on) return;
-    const uint32_t c = chunk_crc(lt, x);
-    if (full) {
-      uint32_t* a = la + j * kBlock + threadIdx.x;
-      *a = shift_tile(lt, *a) ^ c;
-    } else {
-      tail[static_cast<size_t>(j) * kBlock + threadIdx.x] = c;
+  uint32_t* la;    // [k][256] source chains (LDS)
+  uint32_t* ra;    // [U] source chains (registers)
+  uint32_t* tail;  // tail row of source shard 0 of this stripe
+  __device__ __forceinline__ void operator()(int j, const uint4& x) const {
+    if constexpr (FEED != kFeedNone) {
+      const uint32_t c = chunk_crc(lt, x);
+      if constexpr (FEED == kFeedReg) {
+        ra[j] = shift_tile(lt, ra[j]) ^ c;
+      } else if constexpr (FEED == kFeedLds) {
+        uint32_t* a = la + j * kBlock + threadIdx.x;
+        *a = shift_tile(lt, *a) ^ c;
+      } else {
+        tail[static_cast<size_t>(j) * kBlock + threadIdx.x] = c;
+      }
     }
   }
 };
 
-template <int P, int U, int MODE>
-__device__ __forceinline__ void chunk16_crc(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
-                                            int j, long long off, const uint32_t* __restrict__ tbl,
-                                            int len, const SrcCrc& cr) {
-  uint4 x[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
+// acc ^= the U sources x[] (sources j..j+U-1) times their coefficients; each
+// source also feeds its CRC chain.
+template <int P, int U, class Feed>
+__device__ __forceinline__ void mac_feed16(uint32_t (&acc)[P][4], const uint4 (&x)[U], int j,
+                                           const uint32_t* __restrict__ tbl, const Feed& feed) {
   constexpr int PAIR = P <= 4 ? 2 : 1;
 #pragma unroll
   for (int u = 0; u + PAIR <= U; u += PAIR) {
     if constexpr (PAIR == 2) {
       mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
-      cr.feed(j + u, x[u]);
-      cr.feed(j + u + 1, x[u + 1]);
+      feed(j + u, x[u]);
+      feed(j + u + 1, x[u + 1]);
     } else {
       mac16<P>(acc, x[u], tbl + (j + u) * P * kTbl);
-      cr.feed(j + u, x[u]);
+      feed(j + u, x[u]);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (PAIR == 2 && (U & 1)) {
     mac16<P>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl);
-    cr.feed(j + U - 1, x[U - 1]);
+    feed(j + U - 1, x[U - 1]);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-template <int P, class Pol>
-__device__ __forceinline__ void accum16_crc(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
-                                            const uint32_t* __restrict__ tbl, int k, long long off,
-                                            int len, const SrcCrc& cr) {
+template <int U, int MODE>
+__device__ __forceinline__ void load_group(uint4 (&x)[U], const uint64_t* __restrict__ sp, int j,
+                                           long long off, int len) {
 #pragma unroll
-  for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
-  int j = 0;
-  for (; j + Pol::U <= k; j += Pol::U) chunk16_crc<P, Pol::U, Pol::LD>(acc, src, j, off, tbl, len, cr);
-  if constexpr (Pol::U == 4) {
-    if (j + 2 <= k) {
-      chunk16_crc<P, 2, Pol::LD>(acc, src, j, off, tbl, len, cr);
-      j += 2;
-    }
-  }
-  for (; j < k; ++j) chunk16_crc<P, 1, Pol::LD>(acc, src, j, off, tbl, len, cr);
+  for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
 }
 
-template <int P, int U>
+template <int P, int U, int MODE, class Feed>
+__device__ __forceinline__ void chunk16_crc(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
+                                            int j, long long off, const uint32_t* __restrict__ tbl,
+                                            int len, const Feed& feed) {
+  uint4 x[U];
+  load_group<U, MODE>(x, sp, j, off, len);
+  mac_feed16<P, U>(acc, x, j, tbl, feed);
+}
+
+// REG: k == U, one load group whose chains are indexed at compile time.
+template <int P, class Pol, bool REG, class Feed>
+__device__ __forceinline__ void accum16_crc(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
+                                            const uint32_t* __restrict__ tbl, int k, long long off,
+                                            int len, const Feed& feed) {
+#pragma unroll
+  for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
+  if constexpr (REG) {
+    chunk16_crc<P, Pol::U, Pol::LD>(acc, src, 0, off, tbl, len, feed);
+  } else {
+    int j = 0;
+    for (; j + Pol::U <= k; j += Pol::U) chunk16_crc<P, Pol::U, Pol::LD>(acc, src, j, off, tbl, len, feed);
+    if constexpr (Pol::U == 4) {
+      if (j + 2 <= k) {
+        chunk16_crc<P, 2, Pol::LD>(acc, src, j, off, tbl, len, feed);
+        j += 2;
+      }
+    }
+    for (; j < k; ++j) chunk16_crc<P, 1, Pol::LD>(acc, src, j, off, tbl, len, feed);
+  }
+}
+
+template <int P, int U, bool REG>
 constexpr int crc_waves() {
-  constexpr int est = (4 * U + 8 * P + 56 + 7) / 8 * 8;
+  constexpr int est = (4 * U + 8 * P + (REG ? U : 0) + 56 + 7) / 8 * 8;
   constexpr int w = 512 / est;
   return w > 8 ? 8 : (w < 2 ? 2 : w);
 }
 
-template <int P, class Pol>
-__global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U>())) void ec_encode_crc_v16(
+// SRC: this pass also checksums the k sources (the first pass of a stripe).
+template <int P, class Pol, bool REG, bool SRC>
+__global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_encode_crc_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned nblk, unsigned tt,
     unsigned nfull, unsigned ntiles, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part,
-    uint32_t* __restrict__ tail, int nshard_total, int crc_src, int out_shard0) {
+    uint32_t* __restrict__ tail, int nshard_total, int out_shard0) {
+  constexpr int kFull = SRC ? (REG ? kFeedReg : kFeedLds) : kFeedNone;
+  constexpr int kRag = SRC ? kFeedTail : kFeedNone;
+  constexpr int NR = REG ? Pol::U : 1;
   __shared__ uint32_t lt[kCrcTabDw];
-  extern __shared__ uint32_t la[];  // [k][kBlock] when crc_src
+  extern __shared__ uint32_t la[];  // [k][kBlock] when SRC && !REG
   load_crc_tables(lt, tabs);
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned stripe = w / nblk, blk = w - stripe * nblk;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const size_t shard_s = static_cast<size_t>(stripe) * nshard_total;  // source shard 0
     const unsigned t0 = blk * tt, t1 = t0 + tt < ntiles ? t0 + tt : ntiles;
-    uint32_t ao[P];
+    const unsigned tf = t1 < nfull ? t1 : nfull;  // full tiles of this block end here
+    uint32_t ao[P], ra[NR];
 #pragma unroll
     for (int l = 0; l < P; ++l) ao[l] = 0;
-    if (crc_src)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) ra[j] = 0;
+    if constexpr (SRC && !REG)
       for (int j = 0; j < k; ++j) la[j * kBlock + threadIdx.x] = 0;
-    for (unsigned t = t0; t < t1; ++t) {
-      const bool full = t < nfull;
-      const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
-      if (off + kVec <= len) {
-        const SrcCrc cr{lt, la, tail + shard_s * kBlock, crc_src != 0, full};
+    if constexpr (REG) {
+      // Software pipeline: the next tile's sources are in flight while this
+      // tile's GF and CRC work runs (the CRC lookups otherwise leave HBM idle).
+      uint4 xn[Pol::U];
+      if (t0 < tf)
+        load_group<Pol::U, Pol::LD>(xn, sp + src0, 0, static_cast<long long>(t0) * kTile + threadIdx.x * kVec,
+                                    len);
+      for (unsigned t = t0; t < tf; ++t) {
+        const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
+        uint4 x[Pol::U];
+#pragma unroll
+        for (int u = 0; u < Pol::U; ++u) x[u] = xn[u];
+        if (t + 1 < tf) load_group<Pol::U, Pol::LD>(xn, sp + src0, 0, off + kTile, len);
         uint32_t acc[P][4];
-        accum16_crc<P, Pol>(acc, sp + src0, tbl, k, off, len, cr);
+#pragma unroll
+        for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
+        int z = 0;  // opaque zero: see below
+        asm volatile("" : "+s"(z));
+        mac_feed16<P, Pol::U>(acc, x, 0, tbl + z, SrcFeed<kFull>{lt, la, ra, tail + shard_s * kBlock});
 #pragma unroll
         for (int l = 0; l < P; ++l) {
           store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
                            len);
-          const uint32_t c = chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
-          if (full)
-            ao[l] = shift_tile(lt, ao[l]) ^ c;
-          else
-            tail[(shard_s + out_shard0 + l) * kBlock + threadIdx.x] = c;
+          ao[l] = shift_tile(lt, ao[l]) ^ chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
         }
-      } else if (!full) {  // lane past len in the ragged tile (len % 16 == 0)
-        if (crc_src)
-          for (int j = 0; j < k; ++j) tail[(shard_s + j) * kBlock + threadIdx.x] = 0;
+      }
+    } else {
+      for (unsigned t = t0; t < tf; ++t) {
+        const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
+        uint32_t acc[P][4];
+        // An opaque zero offset per tile keeps the compiler from hoisting all
+        // k*P*5 coefficient dwords out of the tile loop (that spills SGPRs).
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        accum16_crc<P, Pol, REG>(acc, sp + src0, tbl + z, k, off, len,
+                                 SrcFeed<kFull>{lt, la, ra, tail + shard_s * kBlock});
 #pragma unroll
-        for (int l = 0; l < P; ++l) tail[(shard_s + out_shard0 + l) * kBlock + threadIdx.x] = 0;
+        for (int l = 0; l < P; ++l) {
+          store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
+                           len);
+          ao[l] = shift_tile(lt, ao[l]) ^ chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+        }
+      }
+    }
+    if (tf < t1) {  // the ragged last tile (t == nfull): len % 16 == 0 here
+      const long long off = static_cast<long long>(tf) * kTile + threadIdx.x * kVec;
+      uint32_t* trow = tail + shard_s * kBlock;
+      if (off + kVec <= len) {
+        uint32_t acc[P][4];
+        accum16_crc<P, Pol, REG>(acc, sp + src0, tbl, k, off, len,
+                                 SrcFeed<kRag>{lt, la, ra, trow});
+#pragma unroll
+        for (int l = 0; l < P; ++l) {
+          store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
+                           len);
+          trow[(out_shard0 + l) * kBlock + threadIdx.x] =
+              chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+        }
+      } else {  // lane past len
+        if constexpr (SRC)
+          for (int j = 0; j < k; ++j) trow[j * kBlock + threadIdx.x] = 0;
+#pragma unroll
+        for (int l = 0; l < P; ++l) trow[(out_shard0 + l) * kBlock + threadIdx.x] = 0;
       }
     }
 #pragma unroll
     for (int l = 0; l < P; ++l)
       part[((shard_s + out_shard0 + l) * nblk + blk) * kBlock + threadIdx.x] = ao[l];
-    if (crc_src)
-      for (int j = 0; j < k; ++j)
-        part[((shard_s + j) * nblk + blk) * kBlock + threadIdx.x] = la[j * kBlock + threadIdx.x];
+    if constexpr (SRC) {
+      if constexpr (REG) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j) part[((shard_s + j) * nblk + blk) * kBlock + threadIdx.x] = ra[j];
+      } else {
+        for (int j = 0; j < k; ++j)
+          part[((shard_s + j) * nblk + blk) * kBlock + threadIdx.x] = la[j * kBlock + threadIdx.x];
+      }
+    }
   }
 }
 
@@ -294,6 +438,12 @@ __global__ __launch_bounds__(kBlock) void crc32c_combine(
 
 constexpr unsigned kMaxCrcItems = 1u << 30;
 
+// Memory policy of the fused kernel: non-temporal global loads/stores (a
+// 64-bit SGPR base per shard instead of a 4-SGPR buffer descriptor: the CRC
+// half needs the scalar registers).
+template <int UU>
+using FusedPol = EncPol<UU, kNT, kNT>;
+
 unsigned crc_grid(unsigned long long nitems) {
   return static_cast<unsigned>(nitems);
 }
@@ -305,16 +455,34 @@ int enc_group_crc(int k) {
   return 4;
 }
 
+// ISAL_HIP_CRC_SRC_CHAIN=lds keeps the source chains in LDS even when the k
+// sources form one load group (tuning knob; default: registers).
+bool src_chain_reg() {
+  static const bool reg = [] {
+    const char* e = getenv("ISAL_HIP_CRC_SRC_CHAIN");
+    return !(e && strcmp(e, "lds") == 0);
+  }();
+  return reg;
+}
+
 template <int P, int U>
 void launch_fused(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
                   int src0, int dst0, const uint32_t* tbl, int len, int k, unsigned nitems,
                   const isal_hip_crc_geom& g, const uint32_t* tabs, uint32_t* part, uint32_t* tail,
                   int nshard_total, int crc_src, int out_shard0) {
-  hipLaunchKernelGGL((ec_encode_crc_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), lds, s, ptrs,
-                     ptr_stride, src0, dst0, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),
-                     static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull),
-                     static_cast<unsigned>(g.ntiles), tabs, part, tail, nshard_total, crc_src,
-                     out_shard0);
+#define FUSED_LAUNCH(REG, SRC, LDS)                                                              \
+  hipLaunchKernelGGL((ec_encode_crc_v16<P, FusedPol<U>, REG, SRC>), dim3(grid), dim3(kBlock), LDS, \
+                     s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems,                         \
+                     static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),                   \
+                     static_cast<unsigned>(g.nfull), static_cast<unsigned>(g.ntiles), tabs, part, \
+                     tail, nshard_total, out_shard0)
+  if (!crc_src)
+    FUSED_LAUNCH(false, false, 0);
+  else if (k == U && src_chain_reg())  // one load group: source chains in registers
+    FUSED_LAUNCH(true, true, 0);
+  else
+    FUSED_LAUNCH(false, true, lds);
+#undef FUSED_LAUNCH
 }
 
 template <int P>

@@ -85,7 +85,18 @@ void isal_hip_count_launch(void);
  * crc32c_combine joins them with the constants of isal_hip_crc32c_plan. */
 #define ISAL_HIP_CRC_TILE 4096
 #define ISAL_HIP_CRC_SLICES 16
-#define ISAL_HIP_CRC_TAB_DWORDS ((ISAL_HIP_CRC_SLICES + 4) * 256)
+/* Kernel lookup tables (isal_hip_crc32c_tables), all indexed by 5-bit fields
+ * so that one table fills the 32 LDS banks exactly once: a wave's lookups
+ * into it never bank-conflict (random byte-indexed tables conflict ~3-way).
+ * Each dword of a 16-byte chunk splits into 7 fields, bits [0,5) [5,10)
+ * [10,15) [15,20) [20,25) [25,30) [30,32):
+ *   [0, 256)                     T0: crc of one byte (bytewise tail loop)
+ *   [256 + (d*7 + f)*32 + v]     crc(0, chunk) of field f of dword d = v
+ *   [256 + 896 + f*32 + v]       Z^4096 of field f of the chain value = v */
+#define ISAL_HIP_CRC_FIELDS 7
+#define ISAL_HIP_CRC_CHUNK_TAB 256
+#define ISAL_HIP_CRC_SHIFT_TAB (ISAL_HIP_CRC_CHUNK_TAB + 4 * ISAL_HIP_CRC_FIELDS * 32)
+#define ISAL_HIP_CRC_TAB_DWORDS (ISAL_HIP_CRC_SHIFT_TAB + ISAL_HIP_CRC_FIELDS * 32)
 #define ISAL_HIP_CRC_PLAN_DWORDS (2 * 1024 + 2 * 256 + 4)
 #define ISAL_HIP_CRC_MAX_FUSED_K 64 /* fused encode keeps k source partials in LDS */
 

@@ -394,6 +394,43 @@ def test_encode_crc_vs_oracle(engine, oracle, gpu, k, rows, n, ns, skew):
     b.close()
 
 
+@pytest.mark.parametrize("tt", [1, 2, 3, 5, 8, 16])
+@pytest.mark.parametrize("k,rows", [(10, 4), (7, 3)])
+def test_encode_crc_tiles_per_workgroup(engine, oracle, gpu, monkeypatch, k, rows, tt):
+    """Every tiles-per-workgroup choice (ISAL_HIP_CRC_TILES) gives the oracle's
+    CRCs: covers the 8-tile batches and their double buffering in the
+    checksum-only kernel (tt >= 8), the one-tile prefetch of the fused kernel,
+    partial last blocks (23 full tiles % tt) and the ragged tile."""
+    import torch
+
+    monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+    n, ns = 4096 * 23 + 2048, 3
+    a = oracle.gf_gen_rs_matrix(k + rows, k)
+    coef = a[k * k:].copy()
+    tbls = engine.ec_init_tables(k, rows, coef)
+    h_data = [[fill_bytes(n, 31 * s + j + tt) for j in range(k)] for s in range(ns)]
+    data = torch.stack([torch.stack([_dev(torch, h_data[s][j], gpu) for j in range(k)]) for s in range(ns)])
+    coding = torch.zeros((ns, rows, n), dtype=torch.uint8, device=gpu)
+    dptr = [int(data[s, j].data_ptr()) for s in range(ns) for j in range(k)]
+    cptr = [int(coding[s, l].data_ptr()) for s in range(ns) for l in range(rows)]
+    crc = torch.zeros(ns * (k + rows), dtype=torch.int32, device=gpu)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.encode_crc(0xFFFFFFFF, crc, 0)
+    torch.cuda.synchronize()
+    got = [int(v) & 0xFFFFFFFF for v in crc.tolist()]
+    for s in range(ns):
+        want = oracle.encode(coef, k, rows, h_data[s])
+        for l in range(rows):
+            assert np.array_equal(_host(coding[s, l]), want[l]), (s, l)
+        for i, buf in enumerate(h_data[s] + want):
+            assert got[s * (k + rows) + i] == oracle.crc32_iscsi(buf, 0xFFFFFFFF), (s, i)
+    crc2 = torch.zeros_like(crc)
+    b.crc(0xFFFFFFFF, crc2, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(crc, crc2)
+    b.close()
+
+
 def test_encode_crc_c2_full_size(engine, oracle, gpu):
     """C2 at full size through the fused path: parity identical to the plain
     encode kernel's, CRCs == oracle on sampled stripes and == the standalone

@@ -33,6 +33,9 @@ for s in $STEPS; do
                 run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
                 grep -E "PASSED|FAILED|SKIPPED|ERROR|passed|failed" "$OUT/pytest_gpu.log" > "$OUT/pytest_gpu_summary.txt" || true
                 ;;
+        tests_crc)
+                run pytest_gpu_crc 300 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
+                ;;
         bench)
                 run bench_c2 300 python bench.py
                 cp "$OUT/bench_c2.log" "$OUT/bench_c2.json"
@@ -65,6 +68,13 @@ for s in $STEPS; do
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_encode.csv" "workload=encode k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encode" "$OUT/pmc_write_encode" ec_encode_v16
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_encode_crc.csv" "workload=encode-crc k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode-crc --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encode-crc" "$OUT/pmc_write_encode-crc" ec_encode_crc_v16
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_crc.csv" "workload=crc k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload crc --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_crc" "$OUT/pmc_write_crc" crc32c_shards
+                ;;
+        pmc_lds)
+                # LDS bank conflicts / VALU pressure of the CRC kernels (one SQ pass each)
+                for wl in ${PMC_WORKLOADS:-crc encode-crc encode}; do
+                        run pmc_lds_$wl 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_$wl" -o l -- python3 bench.py --workload $wl --no-cpu-baseline --steps 2 --warmup 1
+                        run pmc_wait_$wl 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES SQ_INST_CYCLES_VMEM --output-format csv -d "$OUT/pmc_wait_$wl" -o w -- python3 bench.py --workload $wl --no-cpu-baseline --steps 2 --warmup 1
+                done
                 ;;
         probe)
                 run probe 300 isa-l_amd/build/ec_probe
