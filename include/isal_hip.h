@@ -75,6 +75,27 @@ int isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int
                               void *stream);
 int isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream);
 
+/*
+ * CRC64 of every shard: crc[s*(k+rows) + j] as isal_hip_batch_crc, in DEVICE
+ * memory, = crc64_<variant>(init, shard, len) with the reference's semantics
+ * (include/crc64.h:54-163, crc/crc64_base.c:569-670: register starts at ~init,
+ * inverted on return; refl / norm bit order). Variants in the order of
+ * crc64.h. The first call per variant uploads its tables (and synchronises
+ * the device when it replaces another variant's); partials take
+ * nstripes*(k+rows) * ceil(len/65536) * 2 KiB of device memory.
+ */
+#define ISAL_HIP_CRC64_ECMA_REFL 0
+#define ISAL_HIP_CRC64_ECMA_NORM 1
+#define ISAL_HIP_CRC64_ISO_REFL 2
+#define ISAL_HIP_CRC64_ISO_NORM 3
+#define ISAL_HIP_CRC64_JONES_REFL 4
+#define ISAL_HIP_CRC64_JONES_NORM 5
+#define ISAL_HIP_CRC64_ROCKSOFT_REFL 6
+#define ISAL_HIP_CRC64_ROCKSOFT_NORM 7
+#define ISAL_HIP_CRC64_NVARIANTS 8
+int isal_hip_batch_crc64(isal_hip_batch *b, int variant, unsigned long long init,
+                         unsigned long long *crc, void *stream);
+
 /* ---- streaming pipeline for HOST-resident stripes ----------------------- */
 
 /*

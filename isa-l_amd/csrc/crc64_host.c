@@ -1,0 +1,210 @@
+/*
+ * crc64_host.c — host-side tables for the GPU CRC64 kernels (crc64_kernels.hip).
+ *
+ * The eight CRC64 flavours of the reference (include/crc64.h:54-163, algorithm
+ * crc/crc64_base.c:569-670) are table-driven byte loops over a 64-bit register
+ * that starts at ~init and is inverted on return; "refl" shifts right with the
+ * bit-reversed polynomial, "norm" shifts left with the polynomial itself:
+ *   refl: crc = T[(crc ^ b) & 0xff] ^ (crc >> 8)
+ *   norm: crc = T[((crc >> 56) ^ b) & 0xff] ^ (crc << 8)
+ * Without the inversions ("raw") both are GF(2)-linear in (register, data):
+ *   raw(s, A || B) = raw(raw(s, A), B),  raw(s, D) = Z^|D|(s) ^ raw(0, D)
+ * with Z^n = "append n zero bytes", a 64x64 GF(2) matrix. Every constant the
+ * kernels need is such a linear map, so it is built here by evaluating the
+ * bit-serial raw update on basis vectors — one code path for all eight
+ * flavours, no polynomial arithmetic specific to a bit order.
+ *
+ * Linear maps are stored as columns: m[i] = M(e_i); M(v) = XOR of m[i] over the
+ * set bits i of v. On the device a map is applied through "field tables": the
+ * 64-bit input splits into its two dwords, each into 7 fields (bits [0,5)
+ * [5,10) ... [25,30) [30,32)), and table (h, f) holds M(v << (5f + 32h)) for
+ * the 32 values v of the field — 32 entries x 8 B = one 256-byte LDS bank row,
+ * so a wave's ds_read_b64 lookups into one table never bank-conflict.
+ * Nothing here touches shard data.
+ */
+#include <stdint.h>
+#include <string.h>
+
+#include "isal_hip_internal.h"
+
+/* Normal-form polynomials (x^64 implicit) of reference crc64_base.c's tables:
+ * ECMA-182, ISO 3309, Jones, Rocksoft. The refl tables use the bit reversals. */
+static const uint64_t poly_norm[4] = {
+        0x42F0E1EBA9EA3693ULL,
+        0x000000000000001BULL,
+        0xAD93D23594C935A9ULL,
+        0xAD93D23594C93659ULL,
+};
+
+static uint64_t
+bitrev64(uint64_t x)
+{
+        uint64_t r = 0;
+        int i;
+        for (i = 0; i < 64; i++)
+                r |= ((x >> i) & 1) << (63 - i);
+        return r;
+}
+
+int
+isal_hip_crc64_is_refl(int variant)
+{
+        return (variant & 1) == 0; /* ISAL_HIP_CRC64_*_REFL are even */
+}
+
+/* Bit-serial raw update of register s with n bytes (buf NULL: zero bytes). */
+static uint64_t
+raw_update(int variant, uint64_t s, const uint8_t *buf, long long n)
+{
+        const int refl = isal_hip_crc64_is_refl(variant);
+        const uint64_t p = refl ? bitrev64(poly_norm[variant >> 1]) : poly_norm[variant >> 1];
+        long long i;
+        int j;
+        for (i = 0; i < n; i++) {
+                const uint8_t b = buf ? buf[i] : 0;
+                if (refl) {
+                        s ^= b;
+                        for (j = 0; j < 8; j++)
+                                s = (s & 1) ? (s >> 1) ^ p : s >> 1;
+                } else {
+                        s ^= (uint64_t) b << 56;
+                        for (j = 0; j < 8; j++)
+                                s = (s >> 63) ? (s << 1) ^ p : s << 1;
+                }
+        }
+        return s;
+}
+
+static uint64_t
+apply(const uint64_t m[64], uint64_t v)
+{
+        uint64_t r = 0;
+        int i;
+        for (i = 0; i < 64; i++)
+                if (v >> i & 1)
+                        r ^= m[i];
+        return r;
+}
+
+/* c = a ∘ b (apply b first). c may alias neither input. */
+static void
+compose(const uint64_t a[64], const uint64_t b[64], uint64_t c[64])
+{
+        int i;
+        for (i = 0; i < 64; i++)
+                c[i] = apply(a, b[i]);
+}
+
+/* Z^n as columns (square-and-multiply on Z^1). */
+void
+isal_hip_crc64_zpow(int variant, unsigned long long n, uint64_t out[64])
+{
+        uint64_t sq[64], acc[64], t[64];
+        int i;
+        for (i = 0; i < 64; i++) {
+                sq[i] = raw_update(variant, 1ULL << i, NULL, 1);
+                acc[i] = 1ULL << i;
+        }
+        while (n) {
+                if (n & 1) {
+                        compose(sq, acc, t);
+                        memcpy(acc, t, sizeof(t));
+                }
+                n >>= 1;
+                if (n) {
+                        compose(sq, sq, t);
+                        memcpy(sq, t, sizeof(t));
+                }
+        }
+        memcpy(out, acc, sizeof(acc));
+}
+
+static int
+field_lo(int f)
+{
+        return 5 * f;
+}
+
+static uint32_t
+field_mask(int f)
+{
+        return f < ISAL_HIP_CRC_FIELDS - 1 ? 31u : (1u << (32 - 5 * (ISAL_HIP_CRC_FIELDS - 1))) - 1;
+}
+
+/* 14 field tables (448 entries) of the map m. */
+static void
+op_tables(const uint64_t m[64], uint64_t *out)
+{
+        int h, f, v;
+        for (h = 0; h < 2; h++)
+                for (f = 0; f < ISAL_HIP_CRC_FIELDS; f++)
+                        for (v = 0; v < 32; v++)
+                                out[(h * ISAL_HIP_CRC_FIELDS + f) * 32 + v] =
+                                        apply(m, (uint64_t) ((uint32_t) v & field_mask(f))
+                                                         << (field_lo(f) + 32 * h));
+}
+
+/* Layout: isal_hip_internal.h (ISAL_HIP_CRC64_*). */
+void
+isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
+{
+        uint64_t basis[128], m[64];
+        uint8_t chunk[16];
+        isal_hip_crc64_geom g;
+        int b, d, f, v, j, s;
+        isal_hip_crc64_geometry(len, tt, &g);
+        /* byte table of the reference's loop */
+        for (b = 0; b < 256; b++)
+                tabs[ISAL_HIP_CRC64_BYTE_TAB + b] =
+                        raw_update(variant, isal_hip_crc64_is_refl(variant) ? (uint64_t) b
+                                                                              : (uint64_t) b << 56,
+                                   NULL, 1);
+        /* raw(0, 16-byte chunk): bit j of byte i contributes basis[8i + j] */
+        for (j = 0; j < 128; j++) {
+                memset(chunk, 0, sizeof(chunk));
+                chunk[j / 8] = (uint8_t) (1u << (j % 8));
+                basis[j] = raw_update(variant, 0, chunk, 16);
+        }
+        for (d = 0; d < 4; d++)
+                for (f = 0; f < ISAL_HIP_CRC_FIELDS; f++)
+                        for (v = 0; v < 32; v++) {
+                                const uint32_t w = ((uint32_t) v & field_mask(f)) << field_lo(f);
+                                uint64_t c = 0;
+                                for (j = 0; j < 32; j++)
+                                        if (w >> j & 1)
+                                                c ^= basis[32 * d + j]; /* dwords are little-endian */
+                                tabs[ISAL_HIP_CRC64_CHUNK_TAB + (d * ISAL_HIP_CRC_FIELDS + f) * 32 + v] = c;
+                        }
+        isal_hip_crc64_zpow(variant, ISAL_HIP_CRC_TILE, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_SHIFT_TAB);
+        /* combine plan */
+        isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * g.tt, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_OP_BLOCK);
+        isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * g.nfull_last, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_OP_LAST);
+        for (s = 0; s < 8; s++) {
+                isal_hip_crc64_zpow(variant, 16ULL << s, m);
+                op_tables(m, tabs + ISAL_HIP_CRC64_OP_TREE + s * ISAL_HIP_CRC64_OP_ENTRIES);
+        }
+        isal_hip_crc64_zpow(variant, (unsigned long long) (g.tail / 16) * 16, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_OP_TAIL);
+}
+
+void
+isal_hip_crc64_geometry(long long len, int tt, isal_hip_crc64_geom *g)
+{
+        g->nfull = len / ISAL_HIP_CRC_TILE;
+        g->tail = (int) (len % ISAL_HIP_CRC_TILE);
+        g->tt = tt < 1 ? 1 : tt;
+        g->nblk = (g->nfull + g->tt - 1) / g->tt;
+        g->nfull_last = g->nblk ? g->nfull - (g->nblk - 1) * g->tt : 0;
+}
+
+/* Z^len(~init): the register's contribution to crc64(init, buf, len). */
+uint64_t
+isal_hip_crc64_init_term(int variant, long long len, uint64_t init)
+{
+        uint64_t m[64];
+        isal_hip_crc64_zpow(variant, (unsigned long long) len, m);
+        return apply(m, ~init);
+}

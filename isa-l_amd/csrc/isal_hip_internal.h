@@ -109,6 +109,49 @@ typedef struct {
         long long nfull_last; /* full tiles in the last workgroup */
 } isal_hip_crc_geom;
 
+/* ---- CRC64 of shards (crc64_host.c, crc64_kernels.hip) ---------------------
+ * The eight crc64_* flavours (reference include/crc64.h:54-163). Same lane
+ * layout as CRC32C: crc64_shards leaves one 64-bit chain per (shard, block,
+ * lane) over the FULL 4 KiB tiles, part[(shard * nblk + blk) * 256 + L];
+ * crc64_combine folds them, adds the ragged tail read straight from the shard
+ * and the init term. Table buffer (uint64 entries, one per variant and
+ * geometry), every map as 14 field tables of 32 entries (crc64_host.c):
+ *   BYTE_TAB   reference byte table (tail bytes)
+ *   CHUNK_TAB  raw(0, 16-byte chunk), 4 dwords x 7 fields x 32
+ *   SHIFT_TAB  Z^4096                      } crc64_shards loads CHUNK..SHIFT
+ *   OP_BLOCK   Z^(4096*tt)   OP_LAST Z^(4096*nfull_last)
+ *   OP_TREE    Z^(16 * 2^s), s = 0..7 (lane tree)   OP_TAIL Z^(16*(tail/16)) */
+#define ISAL_HIP_CRC64_OP_ENTRIES (2 * ISAL_HIP_CRC_FIELDS * 32)
+#define ISAL_HIP_CRC64_BYTE_TAB 0
+#define ISAL_HIP_CRC64_CHUNK_TAB 256
+#define ISAL_HIP_CRC64_SHIFT_TAB (ISAL_HIP_CRC64_CHUNK_TAB + 4 * ISAL_HIP_CRC_FIELDS * 32)
+#define ISAL_HIP_CRC64_OP_BLOCK (ISAL_HIP_CRC64_SHIFT_TAB + ISAL_HIP_CRC64_OP_ENTRIES)
+#define ISAL_HIP_CRC64_OP_LAST (ISAL_HIP_CRC64_OP_BLOCK + ISAL_HIP_CRC64_OP_ENTRIES)
+#define ISAL_HIP_CRC64_OP_TREE (ISAL_HIP_CRC64_OP_LAST + ISAL_HIP_CRC64_OP_ENTRIES)
+#define ISAL_HIP_CRC64_OP_TAIL (ISAL_HIP_CRC64_OP_TREE + 8 * ISAL_HIP_CRC64_OP_ENTRIES)
+#define ISAL_HIP_CRC64_TAB_ENTRIES (ISAL_HIP_CRC64_OP_TAIL + ISAL_HIP_CRC64_OP_ENTRIES)
+
+typedef struct {
+        long long nfull;      /* full 4 KiB tiles */
+        int tail;             /* bytes after them (< 4096) */
+        int tt;               /* tiles per workgroup */
+        long long nblk;       /* workgroups per shard (0 when nfull == 0) */
+        long long nfull_last; /* full tiles in the last workgroup */
+} isal_hip_crc64_geom;
+
+int isal_hip_crc64_is_refl(int variant);
+void isal_hip_crc64_geometry(long long len, int tt, isal_hip_crc64_geom *g);
+void isal_hip_crc64_zpow(int variant, unsigned long long n, uint64_t out[64]);
+void isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs);
+uint64_t isal_hip_crc64_init_term(int variant, long long len, uint64_t init);
+
+/* crc64(init, shard, len) of the nsh shards of each stripe (d_ptrs row
+ * stride ptr_stride, shards 0..nsh-1) into out[stripe * nsh + i]; init_term =
+ * isal_hip_crc64_init_term(variant, len, init). */
+int isal_hip_launch_crc64(const uint64_t *d_ptrs, int ptr_stride, int nsh, long long nstripes,
+                          int len, int vec16, int refl, int tt, const uint64_t *d_tabs,
+                          uint64_t *d_part, uint64_t init_term, uint64_t *out, void *stream);
+
 uint32_t isal_hip_crc32c_mulmod(uint32_t a, uint32_t b);
 uint32_t isal_hip_crc32c_xpow8n(unsigned long long n);
 void isal_hip_crc32c_tables(uint32_t *tabs);

@@ -569,6 +569,10 @@ struct isal_hip_batch {
          * and the per-lane partials (crc_kernels.hip) */
         isal_hip_crc_geom crc;
         uint32_t *d_crc, *d_part, *d_tail;
+        /* CRC64 state, allocated on first use: the table set of the last
+         * variant used (c64_variant) and the per-lane chains */
+        int c64_variant, c64_tt;
+        uint64_t *d_c64tab, *d_c64part;
 };
 
 int
@@ -679,6 +683,10 @@ isal_hip_batch_destroy(isal_hip_batch *b)
                 (void) hipFree(b->d_crc);
         if (b->d_part)
                 (void) hipFree(b->d_part);
+        if (b->d_c64tab)
+                (void) hipFree(b->d_c64tab);
+        if (b->d_c64part)
+                (void) hipFree(b->d_c64part);
         free(b);
         return ISAL_HIP_OK;
 }
@@ -772,6 +780,65 @@ isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void
                                 b->k + b->rows, 0, stream))
                 return ISAL_HIP_EHIP;
         return batch_crc_finish(b, init, crc, stream);
+}
+
+/* ---- CRC64 of the batch's shards (isal_hip.h) ----------------------------- */
+
+static int
+batch_crc64_setup(isal_hip_batch *b, int variant)
+{
+        isal_hip_crc64_geom g;
+        uint64_t *h;
+        hipError_t e;
+        const size_t tab = ISAL_HIP_CRC64_TAB_ENTRIES;
+        if (b->d_c64tab && b->c64_variant == variant)
+                return ISAL_HIP_OK;
+        if (!b->d_c64tab) {
+                b->c64_tt = crc_tiles(b->len, b->nstripes);
+                isal_hip_crc64_geometry(b->len, b->c64_tt, &g);
+                e = hipMalloc((void **) &b->d_c64tab, tab * 8);
+                if (e == hipSuccess && g.nblk)
+                        e = hipMalloc((void **) &b->d_c64part, (size_t) b->nstripes *
+                                                                       (size_t) (b->k + b->rows) *
+                                                                       (size_t) g.nblk * 256 * 8);
+                if (e != hipSuccess) {
+                        if (b->d_c64tab)
+                                (void) hipFree(b->d_c64tab);
+                        b->d_c64tab = b->d_c64part = NULL;
+                        return e == hipErrorOutOfMemory ? ISAL_HIP_ENOMEM : ISAL_HIP_EHIP;
+                }
+        }
+        h = (uint64_t *) malloc(tab * 8);
+        if (!h)
+                return ISAL_HIP_ENOMEM;
+        isal_hip_crc64_tables(variant, b->len, b->c64_tt, h);
+        /* the previous variant's launches may still read the old tables */
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess)
+                e = hipMemcpy(b->d_c64tab, h, tab * 8, hipMemcpyHostToDevice);
+        free(h);
+        if (e != hipSuccess)
+                return ISAL_HIP_EHIP;
+        b->c64_variant = variant;
+        return ISAL_HIP_OK;
+}
+
+int
+isal_hip_batch_crc64(isal_hip_batch *b, int variant, unsigned long long init,
+                     unsigned long long *crc, void *stream)
+{
+        int r;
+        if (!b || !crc || variant < 0 || variant >= ISAL_HIP_CRC64_NVARIANTS)
+                return ISAL_HIP_EINVAL;
+        if ((r = batch_crc64_setup(b, variant)) != ISAL_HIP_OK)
+                return r;
+        return isal_hip_launch_crc64(b->d_ptrs, b->k + b->rows, b->k + b->rows, b->nstripes,
+                                     b->len, b->vec16, isal_hip_crc64_is_refl(variant), b->c64_tt,
+                                     b->d_c64tab, b->d_c64part,
+                                     isal_hip_crc64_init_term(variant, b->len, init),
+                                     (uint64_t *) crc, stream)
+                       ? ISAL_HIP_EHIP
+                       : ISAL_HIP_OK;
 }
 
 int

@@ -38,6 +38,12 @@ _u8pp = ctypes.POINTER(_u8p)
 _lib = None
 
 
+# Variant numbers of isal_hip_batch_crc64 (ISAL_HIP_CRC64_*): the crc64_*
+# functions of the reference's include/crc64.h, in its order.
+CRC64_VARIANTS = ("ecma_refl", "ecma_norm", "iso_refl", "iso_norm",
+                  "jones_refl", "jones_norm", "rocksoft_refl", "rocksoft_norm")
+
+
 def _one_hip_runtime() -> None:
     """A process must hold exactly ONE HIP runtime. PyTorch-ROCm ships its own
     libamdhip64.so.7; if libisal_hip.so were loaded first it would bind
@@ -93,6 +99,7 @@ def lib() -> ctypes.CDLL:
             "isal_hip_batch_destroy": (i, [ctypes.c_void_p]),
             "isal_hip_batch_encode_crc": (i, [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]),
             "isal_hip_batch_crc": (i, [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]),
+            "isal_hip_batch_crc64": (i, [ctypes.c_void_p, i, ctypes.c_ulonglong, ctypes.c_void_p, ctypes.c_void_p]),
             "isal_hip_pipe_create": (i, [ctypes.POINTER(ctypes.c_void_p), i, i, i, _u8p, i, i]),
             "isal_hip_pipe_submit": (i, [ctypes.c_void_p, _u8pp, _u8pp]),
             "isal_hip_pipe_flush": (i, [ctypes.c_void_p]),
@@ -289,6 +296,15 @@ class Batch:
                                       ctypes.c_void_p(stream))
         if rc != 0:
             raise RuntimeError(f"isal_hip_batch_crc failed ({rc})")
+
+    def crc64(self, variant: int, init: int, crc, stream: int = 0) -> None:
+        """crc64_<variant>(init, shard, len) of every shard into the DEVICE buffer
+        crc (nstripes*(k+rows) 64-bit words, layout as encode_crc()); variant =
+        CRC64_VARIANTS.index(name), the order of the reference's crc64.h."""
+        rc = lib().isal_hip_batch_crc64(self._h, variant, init & 0xFFFFFFFFFFFFFFFF,
+                                        ctypes.c_void_p(addr(crc)), ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_crc64 failed ({rc})")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

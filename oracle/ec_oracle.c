@@ -375,3 +375,62 @@ oracle_crc32_iscsi(const unsigned char *buf, long long len, unsigned int init)
                 crc = (crc >> 8) ^ crc32c_tab[(crc ^ buf[i]) & 0xff];
         return crc;
 }
+
+/* ---- CRC64 (reference crc/crc64_base.c) ----------------------------------- */
+
+/* crc64_base.c:569-670 (crc64_{ecma,iso,jones,rocksoft}_{refl,norm}_base):
+ * crc = ~seed; per byte refl: crc = T[(u8) crc ^ byte] ^ (crc >> 8),
+ * norm: crc = T[((crc >> 56) ^ byte) & 0xff] ^ (crc << 8); return ~crc. The
+ * reference's literal tables (crc64_base.c:32-566) are the byte tables of the
+ * polynomials below (normal form; refl uses the bit reversal); they are
+ * regenerated here. variant = 2 * family + (norm ? 1 : 0), families in the
+ * order of include/crc64.h: ecma, iso, jones, rocksoft. */
+static const unsigned long long crc64_poly[4] = {
+        0x42F0E1EBA9EA3693ULL, 0x000000000000001BULL, 0xAD93D23594C935A9ULL, 0xAD93D23594C93659ULL
+};
+static unsigned long long crc64_tab[8][256];
+static int crc64_ready[8];
+
+static unsigned long long
+rev64(unsigned long long x)
+{
+        unsigned long long r = 0;
+        int i;
+        for (i = 0; i < 64; i++)
+                r |= ((x >> i) & 1ULL) << (63 - i);
+        return r;
+}
+
+unsigned long long
+oracle_crc64(int variant, const unsigned char *buf, long long len, unsigned long long seed)
+{
+        const int norm = variant & 1;
+        unsigned long long crc = ~seed, *t = crc64_tab[variant & 7];
+        long long i;
+        if (!crc64_ready[variant & 7]) {
+                const unsigned long long p = crc64_poly[(variant >> 1) & 3];
+                const unsigned long long pr = rev64(p);
+                int b, k;
+                for (b = 0; b < 256; b++) {
+                        unsigned long long c;
+                        if (norm) {
+                                c = (unsigned long long) b << 56;
+                                for (k = 0; k < 8; k++)
+                                        c = (c >> 63) ? (c << 1) ^ p : c << 1;
+                        } else {
+                                c = (unsigned long long) b;
+                                for (k = 0; k < 8; k++)
+                                        c = (c & 1) ? (c >> 1) ^ pr : c >> 1;
+                        }
+                        t[b] = c;
+                }
+                crc64_ready[variant & 7] = 1;
+        }
+        for (i = 0; i < len; i++) {
+                if (norm)
+                        crc = t[((crc >> 56) ^ buf[i]) & 0xff] ^ (crc << 8);
+                else
+                        crc = t[(crc ^ buf[i]) & 0xff] ^ (crc >> 8);
+        }
+        return ~crc;
+}

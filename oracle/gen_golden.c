@@ -38,6 +38,18 @@ int pq_gen(int vects, int len, void **array);
 int pq_check(int vects, int len, void **array);
 /* Reference crc ABI (reference include/crc.h:137-151; crc/crc_base.c). */
 unsigned int crc32_iscsi_base(unsigned char *buffer, int len, unsigned int crc_init);
+/* Reference crc64 ABI (include/crc64.h:190-330; crc/crc64_base.c:569-670). */
+typedef unsigned long long (*crc64_fn)(unsigned long long, const unsigned char *, unsigned long long);
+unsigned long long crc64_ecma_refl_base(unsigned long long, const unsigned char *, unsigned long long);
+unsigned long long crc64_ecma_norm_base(unsigned long long, const unsigned char *, unsigned long long);
+unsigned long long crc64_iso_refl_base(unsigned long long, const unsigned char *, unsigned long long);
+unsigned long long crc64_iso_norm_base(unsigned long long, const unsigned char *, unsigned long long);
+unsigned long long crc64_jones_refl_base(unsigned long long, const unsigned char *, unsigned long long);
+unsigned long long crc64_jones_norm_base(unsigned long long, const unsigned char *, unsigned long long);
+unsigned long long crc64_rocksoft_refl_base(unsigned long long, const unsigned char *,
+                                            unsigned long long);
+unsigned long long crc64_rocksoft_norm_base(unsigned long long, const unsigned char *,
+                                            unsigned long long);
 
 static FILE *out;
 static int first_item;
@@ -565,6 +577,45 @@ main(int argc, char **argv)
                                         len, inits[ii],
                                         kind == 1 ? "zero" : (kind == 2 ? "8a" : "splitmix"), seed,
                                         crc32_iscsi_base(b, len, inits[ii]));
+                                free(b);
+                        }
+        }
+        fprintf(out, "]");
+
+        /* CRC64, all eight flavours of crc64.h (variant = index below). Same
+         * buffer shapes as crc32_iscsi plus the 16-byte tail boundaries of
+         * the GPU combine. CRC values as decimal strings (64-bit). */
+        fprintf(out, ",\n  \"crc64\": [");
+        first_item = 1;
+        {
+                static const crc64_fn fns[8] = { crc64_ecma_refl_base,    crc64_ecma_norm_base,
+                                                 crc64_iso_refl_base,     crc64_iso_norm_base,
+                                                 crc64_jones_refl_base,   crc64_jones_norm_base,
+                                                 crc64_rocksoft_refl_base, crc64_rocksoft_norm_base };
+                static const int lens[] = { 0, 1, 7, 16, 31, 4095, 4096, 4097, 4112, 4100,
+                                            8192 + 48, 65536 + 4095, 1 << 20 };
+                static const unsigned long long inits[] = { 0ULL, ~0ULL, 0x0123456789abcdefULL };
+                int vi, li, ii;
+                for (vi = 0; vi < 8; vi++)
+                        for (li = 0; li < (int) (sizeof(lens) / sizeof(lens[0])); li++) {
+                                const int len = lens[li];
+                                const unsigned long long seed = 5000 + vi * 97 + li;
+                                unsigned char *b = malloc((size_t) len + 1);
+                                const int kind = (vi + li) % 6 == 0 ? 1 : ((vi + li) % 9 == 0 ? 2 : 0);
+                                ii = (vi + li) % 3;
+                                if (kind == 1)
+                                        memset(b, 0, len);
+                                else if (kind == 2)
+                                        memset(b, 0x8a, len);
+                                else
+                                        fill_bytes(b, len, seed);
+                                item_sep();
+                                fprintf(out,
+                                        "{\"variant\": %d, \"len\": %d, \"init\": \"%llu\", "
+                                        "\"fill\": \"%s\", \"seed\": %llu, \"crc\": \"%llu\"}",
+                                        vi, len, inits[ii],
+                                        kind == 1 ? "zero" : (kind == 2 ? "8a" : "splitmix"), seed,
+                                        fns[vi](inits[ii], b, (unsigned long long) len));
                                 free(b);
                         }
         }

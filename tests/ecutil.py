@@ -88,6 +88,8 @@ class Oracle:
         L.oracle_fnv1a32.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
         L.oracle_crc32_iscsi.restype = ctypes.c_uint
         L.oracle_crc32_iscsi.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_uint]
+        L.oracle_crc64.restype = ctypes.c_ulonglong
+        L.oracle_crc64.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_ulonglong]
         self.L = L
 
     def gf_mul(self, a, b):
@@ -149,6 +151,13 @@ class Oracle:
         a = np.ascontiguousarray(a, dtype=np.uint8)
         return int(self.L.oracle_crc32_iscsi(ctypes.c_void_p(a.ctypes.data), a.size, init & 0xFFFFFFFF))
 
+    def crc64(self, variant: int, a: np.ndarray, init: int) -> int:
+        """crc64_base.c crc64_<variant>_base(init, buf, len) (oracle restatement);
+        variant order of include/crc64.h (ecma/iso/jones/rocksoft x refl/norm)."""
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        return int(self.L.oracle_crc64(variant, ctypes.c_void_p(a.ctypes.data), a.size,
+                                       init & 0xFFFFFFFFFFFFFFFF))
+
     def fnv(self, a: np.ndarray) -> int:
         return int(self.L.oracle_fnv1a32(ctypes.c_void_p(a.ctypes.data), a.size))
 
@@ -177,7 +186,7 @@ def coeffs(gen: str, k: int, rows: int, seed: int, o: Oracle | None = None) -> n
 
 
 def crc_fixture_bytes(entry: dict) -> np.ndarray:
-    """Input buffer of one tests/golden crc32_iscsi entry (gen_golden.c)."""
+    """Input buffer of one tests/golden crc32_iscsi / crc64 entry (gen_golden.c)."""
     n = entry["len"]
     if entry["fill"] == "zero":
         return np.zeros(n, np.uint8)

@@ -254,6 +254,22 @@ def test_oracle_crc32_iscsi(oracle):
     assert oracle.crc32_iscsi(msg, 0xFFFFFFFF) ^ 0xFFFFFFFF == 0xE3069283
 
 
+def test_oracle_crc64(oracle):
+    """oracle restatement of crc64_base.c (all eight crc64_*_base flavours) ==
+    the reference's outputs (tests/golden crc64 section), plus the published
+    check values of the two ECMA-182 conventions."""
+    from ecutil import crc_fixture_bytes
+
+    cases = golden()["crc64"]
+    assert {c["variant"] for c in cases} == set(range(8)) and len(cases) >= 100
+    for case in cases:
+        got = oracle.crc64(case["variant"], crc_fixture_bytes(case), int(case["init"]))
+        assert got == int(case["crc"]), case
+    msg = np.frombuffer(b"123456789", np.uint8)
+    assert oracle.crc64(0, msg, 0) == 0x995DC9BBDF1939FA  # CRC-64/XZ = crc64_ecma_refl(0, .)
+    assert oracle.crc64(1, msg, 0) == 0x62EC59E3F1A4F00A  # CRC-64/WE = crc64_ecma_norm(0, .)
+
+
 def test_simd_port_crc32_iscsi_matches_oracle(oracle):
     """The SSE4.2 crc32 baseline (oracle/ec_gfni_port.c) == oracle crc32_iscsi."""
     import ctypes

@@ -337,6 +337,77 @@ def test_crc_golden_fixtures(engine, oracle, gpu):
         b.close()
 
 
+def _crc64_words(t):
+    return [int(v) & 0xFFFFFFFFFFFFFFFF for v in t.tolist()]
+
+
+def test_crc64_golden_fixtures(engine, oracle, gpu):
+    """isal_hip_batch_crc64 of one shard == the reference's crc64_*_base outputs
+    for all eight flavours (tests/golden crc64: lengths across the 16-byte lane,
+    4 KiB tile and tail boundaries, three init values)."""
+    import torch
+
+    from ecutil import crc_fixture_bytes
+
+    tbls = engine.ec_init_tables(1, 1, np.array([1], np.uint8))
+    out = torch.zeros(2, dtype=torch.int64, device=gpu)
+    for case in golden()["crc64"]:
+        n = case["len"]
+        src = _dev(torch, crc_fixture_bytes(case), gpu) if n else torch.zeros(16, dtype=torch.uint8, device=gpu)
+        dst = torch.zeros(max(n, 16), dtype=torch.uint8, device=gpu)
+        dst[:n] = src[:n]
+        b = engine.Batch(n, 1, 1, tbls, 1, [int(src.data_ptr())], [int(dst.data_ptr())])
+        b.crc64(case["variant"], int(case["init"]), out, 0)
+        torch.cuda.synchronize()
+        assert _crc64_words(out) == [int(case["crc"])] * 2, case
+        b.close()
+
+
+CRC64_SHAPES = [
+    # k, rows, len, nstripes, byte offset of every shard (0: 16-B aligned), tiles/workgroup
+    (10, 4, 65536, 3, 0, None),
+    (4, 2, 4096 * 23 + 2048, 2, 0, 3),   # partial last block, tail of whole chunks
+    (3, 2, 4096 * 5 + 4095, 2, 0, 2),    # tail with 15 loose bytes
+    (2, 1, 4095, 3, 0, None),            # no full tile
+    (3, 3, 4096 * 9 + 77, 2, 3, 4),      # unaligned shards: byte-load kernel
+    (1, 1, 1, 2, 0, None),
+    (5, 2, 4096 * 40, 2, 0, 16),         # several blocks of 16 tiles
+]
+
+
+@pytest.mark.parametrize("variant", range(8))
+@pytest.mark.parametrize("k,rows,n,ns,skew,tt", CRC64_SHAPES)
+def test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, k, rows, n, ns, skew, tt):
+    """crc64_<variant> of every shard of a batch == the oracle, over ragged
+    lengths, unaligned shards and tile-per-workgroup choices; a second variant
+    on the same batch re-uploads the tables."""
+    import torch
+
+    if tt:
+        monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+    a = oracle.gf_gen_rs_matrix(k + rows, k)
+    tbls = engine.ec_init_tables(k, rows, a[k * k:].copy())
+    bufs = [fill_bytes(n, 7919 * s + j + variant) for s in range(ns) for j in range(k + rows)]
+    store = [torch.zeros(n + 32, dtype=torch.uint8, device=gpu) for _ in bufs]
+    for t, h in zip(store, bufs):
+        t[skew:skew + n] = _dev(torch, h, gpu)
+    ptr = [int(t.data_ptr()) + skew for t in store]
+    dptr = [ptr[s * (k + rows) + j] for s in range(ns) for j in range(k)]
+    cptr = [ptr[s * (k + rows) + k + l] for s in range(ns) for l in range(rows)]
+    out = torch.zeros(ns * (k + rows), dtype=torch.int64, device=gpu)
+    init = [0, 0xFFFFFFFFFFFFFFFF, 0x0123456789ABCDEF][variant % 3]
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.crc64(variant, init, out, 0)
+    torch.cuda.synchronize()
+    got = _crc64_words(out)
+    assert got == [oracle.crc64(variant, h, init) for h in bufs]
+    other = (variant + 3) % 8
+    b.crc64(other, init, out, 0)
+    torch.cuda.synchronize()
+    assert _crc64_words(out) == [oracle.crc64(other, h, init) for h in bufs]
+    b.close()
+
+
 CRC_SHAPES = [
     # k, rows, len, nstripes, byte offset of every shard (0: 16-B aligned)
     (10, 4, 65536, 9, 0),             # C2 shape, fused path, tt halving
