@@ -50,7 +50,7 @@ def parse_args(argv=None):
     ap.add_argument("--p", type=int, default=4)
     ap.add_argument("--len", type=int, default=1 << 20, help="shard bytes")
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU per step")
-    ap.add_argument("--workload", choices=["encode", "decode", "update", "encode-crc", "crc",
+    ap.add_argument("--workload", choices=["encode", "decode", "update", "encode-crc", "crc", "crc64",
                                            "e2e-update", "e2e-encode"],
                     default="encode",
                     help="e2e-*: host-resident (pinned) stripes streamed through the pipeline")
@@ -249,7 +249,21 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=Fa
     enc.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.POINTER(u8p), ctypes.POINTER(u8p)]
     enc.restype = None
     crc_fn = None
-    if crc:
+    if crc == "crc64":
+        # crc64_ecma_refl of every shard: the reference's crc64_base.c when built
+        cref = os.path.join(REPO, "oracle", "_ref", "libisal_ref_crc.so")
+        if kind == "reference" and os.path.exists(cref):
+            crc_fn = ctypes.CDLL(cref).crc64_ecma_refl_base
+        else:
+            raw = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so")).oracle_crc64
+            raw.argtypes = [ctypes.c_int, u8p, ctypes.c_longlong, ctypes.c_ulonglong]
+            raw.restype = ctypes.c_ulonglong
+            crc_fn = lambda init, buf, n_: raw(0, buf, n_, init)  # noqa: E731
+        if hasattr(crc_fn, "argtypes"):
+            crc_fn.argtypes = [ctypes.c_ulonglong, u8p, ctypes.c_ulonglong]
+            crc_fn.restype = ctypes.c_ulonglong
+        what = "crc64_ecma_refl of all k+p shards (crc64_base.c)"
+    elif crc:
         # + crc32_iscsi of every shard: the reference's crc_base.c when built
         # (oracle/_ref/libisal_ref_crc.so), else the oracle restatement of it
         cref = os.path.join(REPO, "oracle", "_ref", "libisal_ref_crc.so")
@@ -300,7 +314,10 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=Fa
         while time.perf_counter() < deadline:
             if encode:
                 enc(n, k, p, t, src, dst)  # ctypes drops the GIL for the call
-            if crc_fn is not None:
+            if crc == "crc64":
+                for sh in shards:
+                    crc_fn(0, sh, n)
+            elif crc_fn is not None:
                 for sh in shards:
                     crc_fn(sh, n, 0xFFFFFFFF)
             counts[i] += 1
@@ -402,6 +419,14 @@ def main(argv=None):
                 kernel = "crc32c_shards<true>"
                 workload = (f"CRC32C (crc32_iscsi) of all k+p={k + p} shards, {n} B x {S} "
                             f"stripes/GPU, device-resident")
+        elif args.workload == "crc64":
+            # CRC64 (crc64_ecma_refl, include/crc64.h:55) of all k+p shards
+            crc_out = torch.zeros(S * (k + p), dtype=torch.int64, device=dev)
+            bytes_per_launch = (k + p) * n * S
+            batch.encode(torch.cuda.current_stream(dev).cuda_stream)
+            kernel = "crc64_shards<true>"
+            workload = (f"CRC64 (crc64_ecma_refl) of all k+p={k + p} shards, {n} B x {S} "
+                        f"stripes/GPU, device-resident")
         else:
             bytes_per_launch = (1 + 2 * p) * n * S
             kernel = f"ec_update_v16<{p}>"
@@ -420,6 +445,8 @@ def main(argv=None):
             batch.encode_crc(0xFFFFFFFF, crc_out, h)
         elif args.workload == "crc":
             batch.crc(0xFFFFFFFF, crc_out, h)
+        elif args.workload == "crc64":
+            batch.crc64(0, 0, crc_out, h)
         else:
             batch.encode(h)
 
@@ -454,6 +481,22 @@ def main(argv=None):
             batch.encode_crc(0xFFFFFFFF, crc_ref, h)
         torch.cuda.synchronize(dev)
         ok &= bool(torch.equal(crc_ref, crc_out))
+    if args.workload == "crc64":
+        # CRC64 is affine in the data: crc(x) = L(x) ^ crc(0^n). Parity row 0 is
+        # the XOR of the k sources, so crc(P0) = XOR_j crc(d_j) ^ ((k+1)&1)*crc(0^n).
+        zero = torch.zeros((2, n), dtype=torch.uint8, device=dev)
+        zb = isal_amd.Batch(n, 1, 1, isal_amd.ec_init_tables(1, 1, [1]), 1,
+                            [int(zero[0].data_ptr())], [int(zero[1].data_ptr())])
+        c0 = torch.zeros(2, dtype=torch.int64, device=dev)
+        zb.crc64(0, 0, c0, h)
+        torch.cuda.synchronize(dev)
+        zb.close()
+        got = crc_out.view(S, k + p)
+        for s_ in sorted({0, S // 2, S - 1}):
+            x = int(c0[0]) if (k + 1) & 1 else 0
+            for j in range(k):
+                x ^= int(got[s_, j])
+            ok &= x == int(got[s_, k])
     if args.workload in ("encode", "encode-crc"):
         for s_ in sorted({0, S // 2, S - 1}):
             x = data[s_, 0].clone()
@@ -517,14 +560,15 @@ def main(argv=None):
         check = None
         if args.workload in ("encode", "encode-crc"):
             check = (data[0].cpu().numpy(), out[0].cpu().numpy())
-        with_crc = args.workload in ("encode-crc", "crc")
-        only_crc = args.workload == "crc"
+        with_crc = "crc64" if args.workload == "crc64" else args.workload in ("encode-crc", "crc")
+        only_crc = args.workload in ("crc", "crc64")
         result["cpu_baseline"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check, crc=with_crc,
                                               encode=not only_crc)
         # the reference's fast x86 path cannot be assembled here (no nasm): its
         # AVX-512+GFNI kernels restated in C intrinsics, timed the same way
-        result["cpu_baseline_simd_port"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check,
-                                                        impl="gfni", crc=with_crc, encode=not only_crc)
+        if args.workload != "crc64":  # no SIMD port of the crc64 kernels
+            result["cpu_baseline_simd_port"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check,
+                                                            impl="gfni", crc=with_crc, encode=not only_crc)
     else:
         result["cpu_baseline"] = None
     if d.rank == 0:

@@ -534,6 +534,37 @@ def test_encode_crc_c2_full_size(engine, oracle, gpu):
     b.close()
 
 
+def test_crc64_c2_full_size(engine, oracle, gpu):
+    """CRC64 at the C2 size (1024 stripes x 14 x 1 MiB): sampled stripes ==
+    oracle for a refl and a norm flavour; on all 14336 shards the affine
+    identity crc(P0) = XOR_j crc(d_j) ^ crc(0^n) (k = 10 sources, parity row 0
+    = their XOR) holds."""
+    import torch
+
+    k, p, n, ns = 10, 4, 1 << 20, 1024
+    a = engine.gf_gen_rs_matrix(k + p, k)
+    tbls = engine.ec_init_tables(k, p, a[k * k:])
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, p, n, 91)
+    b = engine.Batch(n, k, p, tbls, ns, dptr, cptr)
+    b.encode(0)
+    crc = torch.zeros(ns * (k + p), dtype=torch.int64, device=gpu)
+    for variant in (0, 5):
+        b.crc64(variant, 0, crc, 0)
+        torch.cuda.synchronize()
+        got = crc.view(ns, k + p)
+        for s in (0, 517, 1023):
+            for i in range(k + p):
+                buf = _host(data[s, i]) if i < k else _host(coding[s, i - k])
+                assert int(got[s, i].item()) & 0xFFFFFFFFFFFFFFFF == oracle.crc64(variant, buf, 0), (variant, s, i)
+        c0 = oracle.crc64(variant, np.zeros(n, np.uint8), 0)
+        x = got[:, 0].clone()
+        for j in range(1, k):
+            x ^= got[:, j]
+        x ^= c0 if c0 < (1 << 63) else c0 - (1 << 64)
+        assert torch.equal(x, got[:, k])
+    b.close()
+
+
 def test_config_c4_streaming_update_k20_p6(engine, oracle, gpu):
     """C4: k=20 p=6, 4 MiB shards, 20 ec_encode_data_update calls into pre-zeroed
     parity == ec_encode_data, and == oracle on a sampled window."""
