@@ -50,7 +50,7 @@ def parse_args(argv=None):
     ap.add_argument("--p", type=int, default=4)
     ap.add_argument("--len", type=int, default=1 << 20, help="shard bytes")
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU per step")
-    ap.add_argument("--workload", choices=["encode", "decode", "update", "encode-crc", "crc", "crc64",
+    ap.add_argument("--workload", choices=["encode", "decode", "update", "encode-crc", "crc", "crc64", "encode-crc64",
                                            "e2e-update", "e2e-encode"],
                     default="encode",
                     help="e2e-*: host-resident (pinned) stripes streamed through the pipeline")
@@ -262,7 +262,8 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=Fa
         if hasattr(crc_fn, "argtypes"):
             crc_fn.argtypes = [ctypes.c_ulonglong, u8p, ctypes.c_ulonglong]
             crc_fn.restype = ctypes.c_ulonglong
-        what = "crc64_ecma_refl of all k+p shards (crc64_base.c)"
+        crc_what = "crc64_ecma_refl of all k+p shards (crc64_base.c)"
+        what = f"ec_encode_data from {what} + {crc_what}" if encode else crc_what
     elif crc:
         # + crc32_iscsi of every shard: the reference's crc_base.c when built
         # (oracle/_ref/libisal_ref_crc.so), else the oracle restatement of it
@@ -419,6 +420,14 @@ def main(argv=None):
                 kernel = "crc32c_shards<true>"
                 workload = (f"CRC32C (crc32_iscsi) of all k+p={k + p} shards, {n} B x {S} "
                             f"stripes/GPU, device-resident")
+        elif args.workload == "encode-crc64":
+            # encode + CRC64 (crc64_ecma_refl) of all k+p shards in one pass
+            crc_out = torch.zeros(S * (k + p), dtype=torch.int64, device=dev)
+            bytes_per_launch = (k + p) * n * S
+            u = enc_group(k)
+            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(k == u).lower()}>"
+            workload = (f"C2 encode + CRC64 (crc64_ecma_refl) of all k+p shards in one pass: k={k} "
+                        f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
         elif args.workload == "crc64":
             # CRC64 (crc64_ecma_refl, include/crc64.h:55) of all k+p shards
             crc_out = torch.zeros(S * (k + p), dtype=torch.int64, device=dev)
@@ -447,6 +456,8 @@ def main(argv=None):
             batch.crc(0xFFFFFFFF, crc_out, h)
         elif args.workload == "crc64":
             batch.crc64(0, 0, crc_out, h)
+        elif args.workload == "encode-crc64":
+            batch.encode_crc64(0, 0, crc_out, h)
         else:
             batch.encode(h)
 
@@ -481,7 +492,13 @@ def main(argv=None):
             batch.encode_crc(0xFFFFFFFF, crc_ref, h)
         torch.cuda.synchronize(dev)
         ok &= bool(torch.equal(crc_ref, crc_out))
-    if args.workload == "crc64":
+    if args.workload == "encode-crc64":
+        # the fused kernel and the standalone CRC64 pass must agree on every shard
+        crc_ref = torch.zeros_like(crc_out)
+        batch.crc64(0, 0, crc_ref, h)
+        torch.cuda.synchronize(dev)
+        ok &= bool(torch.equal(crc_ref, crc_out))
+    if args.workload in ("crc64", "encode-crc64"):
         # CRC64 is affine in the data: crc(x) = L(x) ^ crc(0^n). Parity row 0 is
         # the XOR of the k sources, so crc(P0) = XOR_j crc(d_j) ^ ((k+1)&1)*crc(0^n).
         zero = torch.zeros((2, n), dtype=torch.uint8, device=dev)
@@ -497,7 +514,7 @@ def main(argv=None):
             for j in range(k):
                 x ^= int(got[s_, j])
             ok &= x == int(got[s_, k])
-    if args.workload in ("encode", "encode-crc"):
+    if args.workload in ("encode", "encode-crc", "encode-crc64"):
         for s_ in sorted({0, S // 2, S - 1}):
             x = data[s_, 0].clone()
             for j in range(1, k):
@@ -558,15 +575,15 @@ def main(argv=None):
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         check = None
-        if args.workload in ("encode", "encode-crc"):
+        if args.workload in ("encode", "encode-crc", "encode-crc64"):
             check = (data[0].cpu().numpy(), out[0].cpu().numpy())
-        with_crc = "crc64" if args.workload == "crc64" else args.workload in ("encode-crc", "crc")
+        with_crc = "crc64" if args.workload in ("crc64", "encode-crc64") else args.workload in ("encode-crc", "crc")
         only_crc = args.workload in ("crc", "crc64")
         result["cpu_baseline"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check, crc=with_crc,
                                               encode=not only_crc)
         # the reference's fast x86 path cannot be assembled here (no nasm): its
         # AVX-512+GFNI kernels restated in C intrinsics, timed the same way
-        if args.workload != "crc64":  # no SIMD port of the crc64 kernels
+        if args.workload not in ("crc64", "encode-crc64"):  # no SIMD port of the crc64 kernels
             result["cpu_baseline_simd_port"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check,
                                                             impl="gfni", crc=with_crc, encode=not only_crc)
     else:

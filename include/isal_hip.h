@@ -95,6 +95,12 @@ int isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, 
 #define ISAL_HIP_CRC64_NVARIANTS 8
 int isal_hip_batch_crc64(isal_hip_batch *b, int variant, unsigned long long init,
                          unsigned long long *crc, void *stream);
+/* ec_encode_data for every stripe AND crc64_<variant> of the sources and the
+ * fresh parity (layout as isal_hip_batch_crc64), in one pass over HBM when the
+ * shards are 16-byte aligned, len % 16 == 0, len >= 4096, rows <= 8 and
+ * k <= 32 (otherwise encode, then isal_hip_batch_crc64). */
+int isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long init,
+                                unsigned long long *crc, void *stream);
 
 /* ---- streaming pipeline for HOST-resident stripes ----------------------- */
 

@@ -206,6 +206,213 @@ __global__ __launch_bounds__(kBlock) void crc64_combine(
 
 constexpr unsigned long long kMaxItems = 1ull << 30;
 
+// ---------------------------------------------------------------------------
+// Fused encode + CRC64 (the fragment checksum in the
+// encode pass). The encode half is ec_encode_v16's GF arithmetic on the same
+// 16-byte lane chunks; each source chunk already in registers and each parity
+// chunk about to be stored also feeds its shard's chain
+//   a = Z^4096(a) ^ raw(0, chunk),
+// so the stripe is read and written once. Partials land in crc64_shards'
+// layout (shards 0..k-1 = sources, k..k+P-1 = parity) and crc64_combine
+// finishes them, reading the ragged tail (len % 4096) straight from the
+// shards: the kernel's last block encodes that tile without checksumming it.
+// Source chains live in registers when the k sources form one load group
+// (REG: k == U, e.g. C2's k = 10), else in LDS (lane-private words).
+// ---------------------------------------------------------------------------
+template <int P, int U, class Feed>
+__device__ __forceinline__ void mac_feed(uint32_t (&acc)[P][4], const uint4 (&x)[U], int j,
+                                         const uint32_t* __restrict__ tbl, Feed&& feed) {
+  constexpr int PAIR = P <= 4 ? 2 : 1;
+#pragma unroll
+  for (int u = 0; u + PAIR <= U; u += PAIR) {
+    if constexpr (PAIR == 2) {
+      mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
+      feed(j + u, x[u]);
+      feed(j + u + 1, x[u + 1]);
+    } else {
+      mac16<P>(acc, x[u], tbl + (j + u) * P * kTbl);
+      feed(j + u, x[u]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (PAIR == 2 && (U & 1)) {
+    mac16<P>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl);
+    feed(j + U - 1, x[U - 1]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void load_grp(uint4 (&x)[U], const uint64_t* __restrict__ sp, int j,
+                                         long long off, int len) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) x[u] = load16<kNT>(sp[j + u], off, len);
+}
+
+template <int P, int U, bool REG>
+constexpr int fused64_waves() {
+  constexpr int est = (4 * U * (REG ? 2 : 1) + 6 * P + (REG ? 2 * U : 0) + 88 + 7) / 8 * 8;
+  constexpr int w = 512 / est;
+  return w > 8 ? 8 : (w < 2 ? 2 : w);
+}
+
+template <int P, int U, bool REG>
+__global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encode_crc64_v16(
+    const uint64_t* __restrict__ ptrs, int ptr_stride, const uint32_t* __restrict__ tbl, int len,
+    int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged,
+    const uint64_t* __restrict__ tabs, uint64_t* __restrict__ part) {
+  __shared__ uint64_t lt[kKernTab];
+  extern __shared__ uint64_t la[];  // [k][kBlock] source chains when !REG
+  load_lds<kKernTab>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
+  __syncthreads();
+  const int nsh = k + P;
+  const long long lane = threadIdx.x * kVec;
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned stripe = w / nblk, blk = w - stripe * nblk;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
+    const unsigned t0 = blk * tt, t1 = t0 + tt < nfull ? t0 + tt : nfull;
+    uint64_t ao[P], ra[REG ? U : 1];
+#pragma unroll
+    for (int l = 0; l < P; ++l) ao[l] = 0;
+#pragma unroll
+    for (int j = 0; j < (REG ? U : 1); ++j) ra[j] = 0;
+    if constexpr (!REG)
+      for (int j = 0; j < k; ++j) la[j * kBlock + threadIdx.x] = 0;
+    auto feed = [&](int j, const uint4& x) __attribute__((always_inline)) {
+      const uint64_t c = chunk_crc(lt + kChunk, x.x, x.y, x.z, x.w);
+      if constexpr (REG) {
+        ra[j] = apply_op(lt + kShift, ra[j]) ^ c;
+      } else {
+        uint64_t* a = la + j * kBlock + threadIdx.x;
+        *a = apply_op(lt + kShift, *a) ^ c;
+      }
+    };
+    auto out = [&](uint32_t (&acc)[P][4], long long off) __attribute__((always_inline)) {
+#pragma unroll
+      for (int l = 0; l < P; ++l) {
+        store16<kNT>(sp[k + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
+        ao[l] = apply_op(lt + kShift, ao[l]) ^
+                chunk_crc(lt + kChunk, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+      }
+    };
+    if constexpr (REG) {
+      // the next tile's sources are in flight while this tile's GF and CRC
+      // work runs (the lookups otherwise leave HBM idle)
+      uint4 xn[U];
+      if (t0 < t1) load_grp<U>(xn, sp, 0, static_cast<long long>(t0) * kTile + lane, len);
+      for (unsigned t = t0; t < t1; ++t) {
+        const long long off = static_cast<long long>(t) * kTile + lane;
+        uint4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = xn[u];
+        if (t + 1 < t1) load_grp<U>(xn, sp, 0, off + kTile, len);
+        uint32_t acc[P][4] = {};
+        int z = 0;  // opaque zero: keeps the coefficient loads inside the loop
+        asm volatile("" : "+s"(z));
+        mac_feed<P, U>(acc, x, 0, tbl + z, feed);
+        out(acc, off);
+      }
+    } else {
+      for (unsigned t = t0; t < t1; ++t) {
+        const long long off = static_cast<long long>(t) * kTile + lane;
+        uint32_t acc[P][4] = {};
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        int j = 0;
+        for (; j + U <= k; j += U) {
+          uint4 x[U];
+          load_grp<U>(x, sp, j, off, len);
+          mac_feed<P, U>(acc, x, j, tbl + z, feed);
+        }
+        for (; j < k; ++j) {
+          uint4 x[1];
+          load_grp<1>(x, sp, j, off, len);
+          mac_feed<P, 1>(acc, x, j, tbl + z, feed);
+        }
+        out(acc, off);
+      }
+    }
+    if (ragged && blk + 1 == nblk) {  // encode the tail tile; combine checksums it
+      const long long off = static_cast<long long>(nfull) * kTile + lane;
+      if (off + kVec <= len) {
+        uint32_t acc[P][4] = {};
+        auto none = [](int, const uint4&) {};
+        for (int j = 0; j < k; ++j) {
+          uint4 x[1];
+          load_grp<1>(x, sp, j, off, len);
+          mac_feed<P, 1>(acc, x, j, tbl, none);
+        }
+#pragma unroll
+        for (int l = 0; l < P; ++l)
+          store16<kNT>(sp[k + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
+      }
+    }
+    uint64_t* pp = part + (static_cast<size_t>(stripe) * nsh * nblk + blk) * kBlock + threadIdx.x;
+    const size_t sstep = static_cast<size_t>(nblk) * kBlock;
+    if constexpr (REG) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) pp[j * sstep] = ra[j];
+    } else {
+      for (int j = 0; j < k; ++j) pp[j * sstep] = la[j * kBlock + threadIdx.x];
+    }
+#pragma unroll
+    for (int l = 0; l < P; ++l) pp[(k + l) * sstep] = ao[l];
+  }
+}
+
+int group_u(int k) {
+  static const int cand[] = {12, 10, 8, 6, 5, 4};
+  for (int u : cand)
+    if (k >= u && k % u == 0) return u;
+  return 4;
+}
+
+template <int P, int U>
+void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
+                    const uint32_t* tbl, int len, int k, unsigned nitems,
+                    const isal_hip_crc64_geom& g, const uint64_t* tabs, uint64_t* part) {
+  const int ragged = g.tail != 0;
+  if (k == U)
+    hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, true>), dim3(grid), dim3(kBlock), 0, s, ptrs,
+                       ptr_stride, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),
+                       static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), ragged, tabs, part);
+  else
+    hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, false>), dim3(grid), dim3(kBlock),
+                       static_cast<size_t>(k) * kBlock * 8, s, ptrs, ptr_stride, tbl, len, k, nitems,
+                       static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
+                       static_cast<unsigned>(g.nfull), ragged, tabs, part);
+}
+
+template <int P>
+void fused64_pass(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
+                  const uint32_t* tbl, int len, int k, unsigned nitems,
+                  const isal_hip_crc64_geom& g, const uint64_t* tabs, uint64_t* part) {
+  switch (group_u(k)) {
+#define FUSED64_U(u) \
+  case u: launch_fused64<P, u>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, tabs, part); break;
+    FUSED64_U(12) FUSED64_U(10) FUSED64_U(8) FUSED64_U(6) FUSED64_U(5)
+#undef FUSED64_U
+    default: launch_fused64<P, 4>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, tabs, part);
+  }
+}
+
+int launch_combine64(const uint64_t* part, const uint64_t* ptrs, int ptr_stride, int nsh, int len,
+                     const isal_hip_crc64_geom& g, int refl, const uint64_t* tabs,
+                     uint64_t init_term, uint64_t* out, unsigned nshard, hipStream_t s) {
+  // each combine workgroup copies the 52 KB table set once: cap the grid
+  const unsigned grid = nshard < 2048 ? nshard : 2048;
+  if (refl)
+    hipLaunchKernelGGL(crc64_combine<true>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
+                       nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
+                       tabs, init_term, out, nshard);
+  else
+    hipLaunchKernelGGL(crc64_combine<false>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
+                       nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
+                       tabs, init_term, out, nshard);
+  isal_hip_count_launch();
+  return static_cast<int>(hipGetLastError());
+}
+
 }  // namespace
 
 extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int nsh,
@@ -237,19 +444,46 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return static_cast<int>(e);
     }
-    // each combine workgroup copies the 52 KB table set once: cap the grid
-    const unsigned grid = nshard < 2048 ? nshard : 2048;
-    if (refl)
-      hipLaunchKernelGGL(crc64_combine<true>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
-                         nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
-                         d_tabs, init_term, out + s0 * nsh, nshard);
-    else
-      hipLaunchKernelGGL(crc64_combine<false>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
-                         nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
-                         d_tabs, init_term, out + s0 * nsh, nshard);
+    const int e = launch_combine64(part, ptrs, ptr_stride, nsh, len, g, refl, d_tabs, init_term,
+                                   out + s0 * nsh, nshard, s);
+    if (e) return e;
+  }
+  return 0;
+}
+
+extern "C" int isal_hip_launch_encode_crc64(const uint64_t* d_ptrs, int k, int rows,
+                                            long long nstripes, int len, const uint32_t* d_tbl,
+                                            int refl, int tt, const uint64_t* d_tabs,
+                                            uint64_t* d_part, uint64_t init_term, uint64_t* out,
+                                            void* stream) {
+  if (nstripes <= 0) return 0;
+  isal_hip_crc64_geom g;
+  isal_hip_crc64_geometry(len, tt, &g);
+  if (len % kVec || g.nblk == 0 || rows < 1 || rows > EC_MAX_ROWS_PER_PASS || k < 1 ||
+      k > ISAL_HIP_CRC64_MAX_FUSED_K)
+    return static_cast<int>(hipErrorInvalidValue);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nsh = k + rows;
+  const long long per = static_cast<long long>(kMaxItems / g.nblk) > 0
+                            ? static_cast<long long>(kMaxItems / g.nblk) : 1;
+  for (long long s0 = 0; s0 < nstripes; s0 += per) {
+    const long long ns = nstripes - s0 < per ? nstripes - s0 : per;
+    const unsigned nitems = static_cast<unsigned>(ns * g.nblk);
+    const uint64_t* ptrs = d_ptrs + s0 * nsh;
+    uint64_t* part = d_part + static_cast<size_t>(s0) * nsh * g.nblk * kBlock;
+    switch (rows) {
+#define FUSED64_P(p) \
+  case p: fused64_pass<p>(nitems, s, ptrs, nsh, d_tbl, len, k, nitems, g, d_tabs, part); break;
+      FUSED64_P(1) FUSED64_P(2) FUSED64_P(3) FUSED64_P(4) FUSED64_P(5) FUSED64_P(6) FUSED64_P(7)
+      FUSED64_P(8)
+#undef FUSED64_P
+    }
     isal_hip_count_launch();
-    const hipError_t e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);
+    const int r = launch_combine64(part, ptrs, nsh, nsh, len, g, refl, d_tabs, init_term,
+                                   out + s0 * nsh, static_cast<unsigned>(ns * nsh), s);
+    if (r) return r;
   }
   return 0;
 }

@@ -151,6 +151,15 @@ uint64_t isal_hip_crc64_init_term(int variant, long long len, uint64_t init);
 int isal_hip_launch_crc64(const uint64_t *d_ptrs, int ptr_stride, int nsh, long long nstripes,
                           int len, int vec16, int refl, int tt, const uint64_t *d_tabs,
                           uint64_t *d_part, uint64_t init_term, uint64_t *out, void *stream);
+/* Encode (one pass, rows <= EC_MAX_ROWS_PER_PASS; d_ptrs rows = k sources then
+ * rows parity, stride k + rows) and crc64 of all k + rows shards into
+ * out[stripe * (k + rows) + i]. Needs 16-byte aligned shards, len % 16 == 0,
+ * len >= ISAL_HIP_CRC_TILE and k <= ISAL_HIP_CRC64_MAX_FUSED_K. */
+#define ISAL_HIP_CRC64_MAX_FUSED_K 32 /* source chains: k * 2 KiB of LDS */
+int isal_hip_launch_encode_crc64(const uint64_t *d_ptrs, int k, int rows, long long nstripes,
+                                 int len, const uint32_t *d_tbl, int refl, int tt,
+                                 const uint64_t *d_tabs, uint64_t *d_part, uint64_t init_term,
+                                 uint64_t *out, void *stream);
 
 uint32_t isal_hip_crc32c_mulmod(uint32_t a, uint32_t b);
 uint32_t isal_hip_crc32c_xpow8n(unsigned long long n);

@@ -842,6 +842,33 @@ isal_hip_batch_crc64(isal_hip_batch *b, int variant, unsigned long long init,
 }
 
 int
+isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long init,
+                            unsigned long long *crc, void *stream)
+{
+        int r;
+        isal_hip_crc64_geom g;
+        if (!b || !crc || variant < 0 || variant >= ISAL_HIP_CRC64_NVARIANTS)
+                return ISAL_HIP_EINVAL;
+        if ((r = batch_crc64_setup(b, variant)) != ISAL_HIP_OK)
+                return r;
+        isal_hip_crc64_geometry(b->len, b->c64_tt, &g);
+        if (b->vec16 && b->len % 16 == 0 && g.nblk > 0 && b->rows <= EC_MAX_ROWS_PER_PASS &&
+            b->k <= ISAL_HIP_CRC64_MAX_FUSED_K)
+                /* one pass over the stripe: encode + CRC64 of all k + rows shards */
+                return isal_hip_launch_encode_crc64(
+                               b->d_ptrs, b->k, b->rows, b->nstripes, b->len, b->d_tbl,
+                               isal_hip_crc64_is_refl(variant), b->c64_tt, b->d_c64tab,
+                               b->d_c64part, isal_hip_crc64_init_term(variant, b->len, init),
+                               (uint64_t *) crc, stream)
+                       ? ISAL_HIP_EHIP
+                       : ISAL_HIP_OK;
+        /* unaligned shards, short or ragged len, wide stripes: encode, then CRC64 */
+        if (isal_hip_batch_encode(b, stream) != ISAL_HIP_OK)
+                return ISAL_HIP_EHIP;
+        return isal_hip_batch_crc64(b, variant, init, crc, stream);
+}
+
+int
 isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
 {
         int r;

@@ -100,6 +100,8 @@ def lib() -> ctypes.CDLL:
             "isal_hip_batch_encode_crc": (i, [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]),
             "isal_hip_batch_crc": (i, [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]),
             "isal_hip_batch_crc64": (i, [ctypes.c_void_p, i, ctypes.c_ulonglong, ctypes.c_void_p, ctypes.c_void_p]),
+            "isal_hip_batch_encode_crc64": (i, [ctypes.c_void_p, i, ctypes.c_ulonglong, ctypes.c_void_p,
+                                                ctypes.c_void_p]),
             "isal_hip_pipe_create": (i, [ctypes.POINTER(ctypes.c_void_p), i, i, i, _u8p, i, i]),
             "isal_hip_pipe_submit": (i, [ctypes.c_void_p, _u8pp, _u8pp]),
             "isal_hip_pipe_flush": (i, [ctypes.c_void_p]),
@@ -306,6 +308,14 @@ class Batch:
         if rc != 0:
             raise RuntimeError(f"isal_hip_batch_crc64 failed ({rc})")
 
+    def encode_crc64(self, variant: int, init: int, crc, stream: int = 0) -> None:
+        """encode() plus crc64_<variant>(init, shard, len) of every source and
+        parity shard, layout as crc64(); one pass over HBM where the shape allows."""
+        rc = lib().isal_hip_batch_encode_crc64(self._h, variant, init & 0xFFFFFFFFFFFFFFFF,
+                                               ctypes.c_void_p(addr(crc)), ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_encode_crc64 failed ({rc})")
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             lib().isal_hip_batch_destroy(self._h)
@@ -349,6 +359,14 @@ class Pipe:
         self._keep.clear()
         if rc != 0:
             raise RuntimeError(f"isal_hip_pipe_flush failed ({rc})")
+
+    def encode_crc64(self, variant: int, init: int, crc, stream: int = 0) -> None:
+        """encode() plus crc64_<variant>(init, shard, len) of every source and
+        parity shard, layout as crc64(); one pass over HBM where the shape allows."""
+        rc = lib().isal_hip_batch_encode_crc64(self._h, variant, init & 0xFFFFFFFFFFFFFFFF,
+                                               ctypes.c_void_p(addr(crc)), ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_encode_crc64 failed ({rc})")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

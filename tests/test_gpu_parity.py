@@ -565,6 +565,92 @@ def test_crc64_c2_full_size(engine, oracle, gpu):
     b.close()
 
 
+ENCODE_CRC64_SHAPES = [
+    # k, rows, len, nstripes, byte offset of every shard, tiles/workgroup, variant
+    (10, 4, 65536, 5, 0, None, 0),        # C2 shape: source chains in registers
+    (10, 4, 4096 * 37 + 2048, 3, 0, 4, 1),  # ragged tile encoded by the last block
+    (7, 3, 4096 * 20, 2, 0, 3, 2),        # k % U != 0: LDS source chains
+    (12, 8, 4096 * 9 + 160, 2, 0, 2, 5),  # rows = 8, one group of 12
+    (20, 6, 4096 * 6, 2, 0, None, 7),     # k > U: two load groups, LDS chains
+    (4, 10, 4096 * 3, 2, 0, None, 4),     # rows > 8 -> encode, then CRC64
+    (3, 2, 4096 * 2 + 13, 2, 0, None, 3), # len % 16 != 0 -> encode, then CRC64
+    (5, 2, 3000, 3, 0, None, 6),          # no full tile -> encode, then CRC64
+    (4, 3, 4096 * 4, 2, 5, None, 0),      # unaligned shards -> encode, then CRC64
+]
+
+
+@pytest.mark.parametrize("k,rows,n,ns,skew,tt,variant", ENCODE_CRC64_SHAPES)
+def test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant):
+    """Fused encode + CRC64 (isal_hip_batch_encode_crc64): parity == oracle
+    encode, every shard's crc64_<variant> == oracle; the fallback shapes agree
+    through encode-then-CRC64."""
+    import torch
+
+    if tt:
+        monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+    a = oracle.gf_gen_rs_matrix(k + rows, k)
+    coef = a[k * k:].copy()
+    tbls = engine.ec_init_tables(k, rows, coef)
+    stride = n + 64
+    pool = torch.zeros(ns * (k + rows) * stride + 64, dtype=torch.uint8, device=gpu)
+    h_data = [[fill_bytes(n, 13 * s + j + n + variant) for j in range(k)] for s in range(ns)]
+
+    def at(s, i):
+        return (s * (k + rows) + i) * stride + skew
+
+    for s in range(ns):
+        for j in range(k):
+            pool[at(s, j):at(s, j) + n] = _dev(torch, h_data[s][j], gpu)
+    base = int(pool.data_ptr())
+    dptr = [base + at(s, j) for s in range(ns) for j in range(k)]
+    cptr = [base + at(s, k + l) for s in range(ns) for l in range(rows)]
+    init = [0, 0xFFFFFFFFFFFFFFFF, 0x0123456789ABCDEF][variant % 3]
+    out = torch.zeros(ns * (k + rows), dtype=torch.int64, device=gpu)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.encode_crc64(variant, init, out, 0)
+    torch.cuda.synchronize()
+    h_pool, got = _host(pool), _crc64_words(out)
+    for s in range(ns):
+        want = oracle.encode(coef, k, rows, h_data[s])
+        for l in range(rows):
+            assert np.array_equal(h_pool[at(s, k + l):at(s, k + l) + n], want[l]), (s, l)
+        for i, buf in enumerate(h_data[s] + want):
+            assert got[s * (k + rows) + i] == oracle.crc64(variant, buf, init), (s, i)
+    b.close()
+
+
+def test_encode_crc64_c2_full_size(engine, oracle, gpu):
+    """C2 at full size through the fused encode + CRC64 pass: parity identical
+    to the plain encode kernel's, CRC64s == the standalone CRC64 pass on all
+    14336 shards and == oracle on sampled stripes."""
+    import torch
+
+    k, p, n, ns = 10, 4, 1 << 20, 1024
+    a = engine.gf_gen_rs_matrix(k + p, k)
+    tbls = engine.ec_init_tables(k, p, a[k * k:])
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, p, n, 53)
+    b = engine.Batch(n, k, p, tbls, ns, dptr, cptr)
+    b.encode(0)
+    torch.cuda.synchronize()
+    ref = coding.clone()
+    coding.zero_()
+    crc = torch.zeros(ns * (k + p), dtype=torch.int64, device=gpu)
+    b.encode_crc64(0, 0, crc, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(coding, ref)
+    del ref
+    crc2 = torch.zeros_like(crc)
+    b.crc64(0, 0, crc2, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(crc, crc2)
+    got = crc.view(ns, k + p)
+    for s in (0, 700, 1023):
+        for i in range(k + p):
+            buf = _host(data[s, i]) if i < k else _host(coding[s, i - k])
+            assert int(got[s, i].item()) & 0xFFFFFFFFFFFFFFFF == oracle.crc64(0, buf, 0), (s, i)
+    b.close()
+
+
 def test_config_c4_streaming_update_k20_p6(engine, oracle, gpu):
     """C4: k=20 p=6, 4 MiB shards, 20 ec_encode_data_update calls into pre-zeroed
     parity == ec_encode_data, and == oracle on a sampled window."""

@@ -53,6 +53,14 @@ for s in $STEPS; do
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_crc64.csv" "workload=crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_crc64" "$OUT/pmc_write_crc64" crc64_shards
                 run pmc_lds_crc64 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_crc64" -o l -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 2 --warmup 1
                 ;;
+        encrc64)
+                run pytest_gpu_encrc64 300 python -u -m pytest tests -m gpu -x -v -k "encode_crc64" --timeout 200 --timeout-method thread
+                run bench_encode_crc64 300 python bench.py --workload encode-crc64 --cpu-seconds 5
+                run rocprof_encrc64 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_encrc64" -o encrc64 -- python3 bench.py --workload encode-crc64 --no-cpu-baseline
+                run pmc_fetch_encrc64 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_encrc64" -o f -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 3 --warmup 1
+                run pmc_write_encrc64 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_encrc64" -o w -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 3 --warmup 1
+                python3 tools/pmc_csv.py "$OUT/pmc_c2_encode_crc64.csv" "workload=encode-crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode-crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encrc64" "$OUT/pmc_write_encrc64" ec_encode_crc64_v16
+                ;;
         decode)
                 run bench_decode 300 python bench.py --workload decode --no-cpu-baseline
                 ;;
