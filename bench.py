@@ -433,7 +433,7 @@ def main(argv=None):
             crc_out = torch.zeros(S * (k + p), dtype=torch.int64, device=dev)
             bytes_per_launch = (k + p) * n * S
             batch.encode(torch.cuda.current_stream(dev).cuda_stream)
-            kernel = "crc64_shards<true>"
+            kernel = "crc64_shards<true, 2, 4>"
             workload = (f"CRC64 (crc64_ecma_refl) of all k+p={k + p} shards, {n} B x {S} "
                         f"stripes/GPU, device-resident")
         else:

@@ -144,6 +144,24 @@ op_tables(const uint64_t m[64], uint64_t *out)
                                                          << (field_lo(f) + 32 * h));
 }
 
+/* 28 field tables of the map chunk -> XOR of basis[bit] (bit j of dword d of
+ * the chunk contributes basis[32 * d + j]; dwords are little-endian). */
+static void
+chunk_tables(const uint64_t basis[128], uint64_t *out)
+{
+        int d, f, v, j;
+        for (d = 0; d < 4; d++)
+                for (f = 0; f < ISAL_HIP_CRC_FIELDS; f++)
+                        for (v = 0; v < 32; v++) {
+                                const uint32_t w = ((uint32_t) v & field_mask(f)) << field_lo(f);
+                                uint64_t c = 0;
+                                for (j = 0; j < 32; j++)
+                                        if (w >> j & 1)
+                                                c ^= basis[32 * d + j];
+                                out[(d * ISAL_HIP_CRC_FIELDS + f) * 32 + v] = c;
+                        }
+}
+
 /* Layout: isal_hip_internal.h (ISAL_HIP_CRC64_*). */
 void
 isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
@@ -151,7 +169,7 @@ isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
         uint64_t basis[128], m[64];
         uint8_t chunk[16];
         isal_hip_crc64_geom g;
-        int b, d, f, v, j, s;
+        int b, j, s;
         isal_hip_crc64_geometry(len, tt, &g);
         /* byte table of the reference's loop */
         for (b = 0; b < 256; b++)
@@ -165,18 +183,22 @@ isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
                 chunk[j / 8] = (uint8_t) (1u << (j % 8));
                 basis[j] = raw_update(variant, 0, chunk, 16);
         }
-        for (d = 0; d < 4; d++)
-                for (f = 0; f < ISAL_HIP_CRC_FIELDS; f++)
-                        for (v = 0; v < 32; v++) {
-                                const uint32_t w = ((uint32_t) v & field_mask(f)) << field_lo(f);
-                                uint64_t c = 0;
-                                for (j = 0; j < 32; j++)
-                                        if (w >> j & 1)
-                                                c ^= basis[32 * d + j]; /* dwords are little-endian */
-                                tabs[ISAL_HIP_CRC64_CHUNK_TAB + (d * ISAL_HIP_CRC_FIELDS + f) * 32 + v] = c;
-                        }
+        chunk_tables(basis, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
         isal_hip_crc64_zpow(variant, ISAL_HIP_CRC_TILE, m);
         op_tables(m, tabs + ISAL_HIP_CRC64_SHIFT_TAB);
+        /* multi-tile chain step: chunk maps followed by m tiles, Z^(4096*2), Z^(4096*4) */
+        for (s = 1; s <= 3; s++) {
+                uint64_t bm[128];
+                isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * s, m);
+                for (j = 0; j < 128; j++)
+                        bm[j] = apply(m, basis[j]);
+                chunk_tables(bm, tabs + ISAL_HIP_CRC64_CHUNKX_TAB +
+                                         (s - 1) * ISAL_HIP_CRC64_CHUNK_ENTRIES);
+        }
+        isal_hip_crc64_zpow(variant, 2ULL * ISAL_HIP_CRC_TILE, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_SHIFTX_TAB);
+        isal_hip_crc64_zpow(variant, 4ULL * ISAL_HIP_CRC_TILE, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_SHIFTX_TAB + ISAL_HIP_CRC64_OP_ENTRIES);
         /* combine plan */
         isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * g.tt, m);
         op_tables(m, tabs + ISAL_HIP_CRC64_OP_BLOCK);

@@ -12,6 +12,7 @@
 // the last < 16 bytes knows the shift direction (REFL).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ec_device.h"
 
@@ -89,20 +90,43 @@ __device__ __forceinline__ void load_lds(uint64_t* dst, const uint64_t* __restri
   for (int i = threadIdx.x; i < N / 2; i += kBlock) d[i] = s[i];
 }
 
-constexpr unsigned kBatch = 4;  // full tiles whose loads are issued together
+constexpr int kBatch = 4;  // full tiles whose loads are issued together (default)
+constexpr int kCE = ISAL_HIP_CRC64_CHUNK_ENTRIES;
+
+// LDS layout of crc64_shards<VEC, M>: chunk map (m = 0) and Z^4096 [kKernTab],
+// the chunk maps followed by m = 1..M-1 tiles, Z^(4096*M).
+template <int M>
+constexpr int shards_lds() {
+  return kKernTab + (M > 1 ? (M - 1) * kCE + kOp : 0);
+}
+template <int M>
+__device__ __forceinline__ const uint64_t* chunk_map(const uint64_t* lt, int m) {
+  return m == 0 ? lt + kChunk : lt + kKernTab + (m - 1) * kCE;
+}
 
 // Chains of the full tiles. Item = (stripe, shard, block), shard-major within
 // a stripe: part index = ((stripe * nsh + i) * nblk + blk) * 256 + L.
-template <bool VEC>
+// M > 1 advances the chain M tiles per step,
+//   a = Z^(4096*M)(a) ^ XOR_h (Z^(4096*(M-1-h)) o raw(0, .))(chunk_h),
+// with the shifted chunk maps precomputed: 14 + 28*M lookups per M tiles
+// instead of 42*M (M = 4: -25 %).
+template <bool VEC, int M, int B = kBatch>
 __global__ __launch_bounds__(kBlock) void crc64_shards(const uint64_t* __restrict__ ptrs,
                                                        int ptr_stride, int nsh, int len,
                                                        unsigned nitems, unsigned nblk, unsigned tt,
                                                        unsigned nfull,
                                                        const uint64_t* __restrict__ tabs,
                                                        uint64_t* __restrict__ part) {
-  __shared__ uint64_t lt[kKernTab];
+  static_assert(B % M == 0, "chain step divides the load batch");
+  __shared__ uint64_t lt[shards_lds<M>()];
   load_lds<kKernTab>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
+  if constexpr (M > 1) {
+    load_lds<(M - 1) * kCE>(lt + kKernTab, tabs + ISAL_HIP_CRC64_CHUNKX_TAB);
+    load_lds<kOp>(lt + kKernTab + (M - 1) * kCE,
+                  tabs + ISAL_HIP_CRC64_SHIFTX_TAB + (M == 4 ? kOp : 0));
+  }
   __syncthreads();
+  const uint64_t* shift_m = M > 1 ? lt + kKernTab + (M - 1) * kCE : lt + kShift;
   const long long lane = threadIdx.x * kVec;
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned si = w / nblk, blk = w - si * nblk;
@@ -112,14 +136,20 @@ __global__ __launch_bounds__(kBlock) void crc64_shards(const uint64_t* __restric
     uint64_t a = 0;
     unsigned t = t0;
     if constexpr (VEC) {
-      for (; t + kBatch <= t1; t += kBatch) {
-        uint4 x[kBatch];
+      for (; t + B <= t1; t += B) {
+        uint4 x[B];
 #pragma unroll
-        for (unsigned g = 0; g < kBatch; ++g)
+        for (unsigned g = 0; g < B; ++g)
           x[g] = load16<kBufNT>(base, static_cast<long long>(t + g) * kTile + lane, len);
 #pragma unroll
-        for (unsigned g = 0; g < kBatch; ++g)
-          a = apply_op(lt + kShift, a) ^ chunk_crc(lt + kChunk, x[g].x, x[g].y, x[g].z, x[g].w);
+        for (unsigned g = 0; g < B; g += M) {
+          uint64_t c = 0;
+#pragma unroll
+          for (int h = 0; h < M; ++h)
+            c ^= chunk_crc(chunk_map<M>(lt, M - 1 - h), x[g + h].x, x[g + h].y, x[g + h].z,
+                           x[g + h].w);
+          a = apply_op(shift_m, a) ^ c;
+        }
       }
       for (; t < t1; ++t) {
         const uint4 x = load16<kBufNT>(base, static_cast<long long>(t) * kTile + lane, len);
@@ -160,9 +190,9 @@ __global__ __launch_bounds__(kBlock) void crc64_combine(
     const uint64_t* __restrict__ part, const uint64_t* __restrict__ ptrs, int ptr_stride, int nsh,
     int len, unsigned nblk, unsigned nfull, const uint64_t* __restrict__ tabs, uint64_t init_term,
     uint64_t* __restrict__ out, unsigned nshard_total) {
-  __shared__ uint64_t lt[ISAL_HIP_CRC64_TAB_ENTRIES];
+  __shared__ uint64_t lt[ISAL_HIP_CRC64_COMBINE_ENTRIES];
   __shared__ uint64_t red[kBlock];
-  load_lds<ISAL_HIP_CRC64_TAB_ENTRIES>(lt, tabs);
+  load_lds<ISAL_HIP_CRC64_COMBINE_ENTRIES>(lt, tabs);
   __syncthreads();
   const int tail = len - static_cast<int>(nfull) * kTile;
   const int q = tail / kVec, rem = tail - q * kVec;
@@ -205,6 +235,21 @@ __global__ __launch_bounds__(kBlock) void crc64_combine(
 }
 
 constexpr unsigned long long kMaxItems = 1ull << 30;
+
+// Tiles per chain step of crc64_shards (ISAL_HIP_CRC64_STEP = 1, 2 or 4).
+// Measured on the C2 shape (profiles/r01_crc64_step_sweep.txt): 2 tiles per
+// step with 4 loads in flight is fastest; 4 per step costs occupancy (LDS).
+int chain_step() {
+  const char* e = getenv("ISAL_HIP_CRC64_STEP");
+  const int v = e ? atoi(e) : 2;
+  return v == 1 || v == 4 ? v : 2;
+}
+
+// Full tiles loaded per batch (ISAL_HIP_CRC64_BATCH = 4 or 8).
+int load_batch() {
+  const char* e = getenv("ISAL_HIP_CRC64_BATCH");
+  return e && atoi(e) == 8 ? 8 : 4;
+}
 
 // ---------------------------------------------------------------------------
 // Fused encode + CRC64 (the fragment checksum in the
@@ -432,14 +477,20 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
     uint64_t* part = d_part + static_cast<size_t>(s0) * nsh * g.nblk * kBlock;
     if (g.nblk) {
       const unsigned nitems = static_cast<unsigned>(ns * nsh * g.nblk);
-      if (vec16)
-        hipLaunchKernelGGL(crc64_shards<true>, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride,
-                           nsh, len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
-                           static_cast<unsigned>(g.nfull), d_tabs, part);
+#define SHARDS_LAUNCH(V, M, B)                                                                \
+  hipLaunchKernelGGL((crc64_shards<V, M, B>), dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, \
+                     len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),      \
+                     static_cast<unsigned>(g.nfull), d_tabs, part)
+      const int m = chain_step(), b8 = load_batch() == 8;
+      if (!vec16)
+        SHARDS_LAUNCH(false, 1, 4);
+      else if (m == 4)
+        { if (b8) SHARDS_LAUNCH(true, 4, 8); else SHARDS_LAUNCH(true, 4, 4); }
+      else if (m == 2)
+        { if (b8) SHARDS_LAUNCH(true, 2, 8); else SHARDS_LAUNCH(true, 2, 4); }
       else
-        hipLaunchKernelGGL(crc64_shards<false>, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride,
-                           nsh, len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
-                           static_cast<unsigned>(g.nfull), d_tabs, part);
+        { if (b8) SHARDS_LAUNCH(true, 1, 8); else SHARDS_LAUNCH(true, 1, 4); }
+#undef SHARDS_LAUNCH
       isal_hip_count_launch();
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return static_cast<int>(e);

@@ -120,7 +120,10 @@ typedef struct {
  *   CHUNK_TAB  raw(0, 16-byte chunk), 4 dwords x 7 fields x 32
  *   SHIFT_TAB  Z^4096                      } crc64_shards loads CHUNK..SHIFT
  *   OP_BLOCK   Z^(4096*tt)   OP_LAST Z^(4096*nfull_last)
- *   OP_TREE    Z^(16 * 2^s), s = 0..7 (lane tree)   OP_TAIL Z^(16*(tail/16)) */
+ *   OP_TREE    Z^(16 * 2^s), s = 0..7 (lane tree)   OP_TAIL Z^(16*(tail/16))
+ *   (crc64_combine loads BYTE..OP_TAIL: COMBINE_ENTRIES)
+ *   CHUNKX_TAB Z^(4096*m) o raw(0, chunk), m = 1..3 (multi-tile chain step)
+ *   SHIFTX_TAB Z^8192, Z^16384 */
 #define ISAL_HIP_CRC64_OP_ENTRIES (2 * ISAL_HIP_CRC_FIELDS * 32)
 #define ISAL_HIP_CRC64_BYTE_TAB 0
 #define ISAL_HIP_CRC64_CHUNK_TAB 256
@@ -129,7 +132,11 @@ typedef struct {
 #define ISAL_HIP_CRC64_OP_LAST (ISAL_HIP_CRC64_OP_BLOCK + ISAL_HIP_CRC64_OP_ENTRIES)
 #define ISAL_HIP_CRC64_OP_TREE (ISAL_HIP_CRC64_OP_LAST + ISAL_HIP_CRC64_OP_ENTRIES)
 #define ISAL_HIP_CRC64_OP_TAIL (ISAL_HIP_CRC64_OP_TREE + 8 * ISAL_HIP_CRC64_OP_ENTRIES)
-#define ISAL_HIP_CRC64_TAB_ENTRIES (ISAL_HIP_CRC64_OP_TAIL + ISAL_HIP_CRC64_OP_ENTRIES)
+#define ISAL_HIP_CRC64_COMBINE_ENTRIES (ISAL_HIP_CRC64_OP_TAIL + ISAL_HIP_CRC64_OP_ENTRIES)
+#define ISAL_HIP_CRC64_CHUNK_ENTRIES (4 * ISAL_HIP_CRC_FIELDS * 32)
+#define ISAL_HIP_CRC64_CHUNKX_TAB ISAL_HIP_CRC64_COMBINE_ENTRIES
+#define ISAL_HIP_CRC64_SHIFTX_TAB (ISAL_HIP_CRC64_CHUNKX_TAB + 3 * ISAL_HIP_CRC64_CHUNK_ENTRIES)
+#define ISAL_HIP_CRC64_TAB_ENTRIES (ISAL_HIP_CRC64_SHIFTX_TAB + 2 * ISAL_HIP_CRC64_OP_ENTRIES)
 
 typedef struct {
         long long nfull;      /* full 4 KiB tiles */

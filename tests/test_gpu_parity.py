@@ -565,6 +565,36 @@ def test_crc64_c2_full_size(engine, oracle, gpu):
     b.close()
 
 
+@pytest.mark.parametrize("batch", [4, 8])
+@pytest.mark.parametrize("step", [1, 2, 4])
+@pytest.mark.parametrize("k,rows,n,ns,skew,tt", [CRC64_SHAPES[0], CRC64_SHAPES[1], CRC64_SHAPES[6],
+                                                 (3, 1, 4096 * 11 + 16, 2, 0, 7)])
+def test_crc64_chain_step(engine, oracle, gpu, monkeypatch, step, batch, k, rows, n, ns, skew, tt):
+    """crc64_shards advancing its chain 1, 2 or 4 tiles per step (shifted chunk
+    maps, ISAL_HIP_CRC64_STEP), 4 or 8 tile loads in flight, == oracle, incl. blocks whose tile count is not
+    a multiple of the step."""
+    import torch
+
+    monkeypatch.setenv("ISAL_HIP_CRC64_STEP", str(step))
+    monkeypatch.setenv("ISAL_HIP_CRC64_BATCH", str(batch))
+    if tt:
+        monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+    a = oracle.gf_gen_rs_matrix(k + rows, k)
+    tbls = engine.ec_init_tables(k, rows, a[k * k:].copy())
+    bufs = [fill_bytes(n, 31 * s + j + step) for s in range(ns) for j in range(k + rows)]
+    store = [_dev(torch, h, gpu) for h in bufs]
+    ptr = [int(t.data_ptr()) for t in store]
+    dptr = [ptr[s * (k + rows) + j] for s in range(ns) for j in range(k)]
+    cptr = [ptr[s * (k + rows) + k + l] for s in range(ns) for l in range(rows)]
+    out = torch.zeros(ns * (k + rows), dtype=torch.int64, device=gpu)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    for variant in (0, 3):
+        b.crc64(variant, 0x5A5A, out, 0)
+        torch.cuda.synchronize()
+        assert _crc64_words(out) == [oracle.crc64(variant, h, 0x5A5A) for h in bufs], variant
+    b.close()
+
+
 ENCODE_CRC64_SHAPES = [
     # k, rows, len, nstripes, byte offset of every shard, tiles/workgroup, variant
     (10, 4, 65536, 5, 0, None, 0),        # C2 shape: source chains in registers

@@ -61,6 +61,17 @@ for s in $STEPS; do
                 run pmc_write_encrc64 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_encrc64" -o w -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 3 --warmup 1
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_encode_crc64.csv" "workload=encode-crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode-crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encrc64" "$OUT/pmc_write_encrc64" ec_encode_crc64_v16
                 ;;
+        crc64step)
+                run pytest_gpu_crc64 300 python -u -m pytest tests -m gpu -x -v -k "crc64" --timeout 200 --timeout-method thread
+                for mb in 1:4 2:4 4:4 1:8 2:8 4:8; do
+                        ISAL_HIP_CRC64_STEP=${mb%:*} ISAL_HIP_CRC64_BATCH=${mb#*:} run bench_crc64_step${mb/:/_b} 300 python bench.py --workload crc64 --no-cpu-baseline
+                done
+                run bench_crc64 300 python bench.py --workload crc64 --cpu-seconds 5
+                run rocprof_crc64 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_crc64" -o crc64 -- python3 bench.py --workload crc64 --no-cpu-baseline
+                run pmc_fetch_crc64 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_crc64" -o f -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 3 --warmup 1
+                run pmc_write_crc64 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_crc64" -o w -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 3 --warmup 1
+                python3 tools/pmc_csv.py "$OUT/pmc_c2_crc64.csv" "workload=crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_crc64" "$OUT/pmc_write_crc64" crc64_shards
+                ;;
         decode)
                 run bench_decode 300 python bench.py --workload decode --no-cpu-baseline
                 ;;
