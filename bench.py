@@ -425,7 +425,8 @@ def main(argv=None):
             crc_out = torch.zeros(S * (k + p), dtype=torch.int64, device=dev)
             bytes_per_launch = (k + p) * n * S
             u = enc_group(k)
-            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(k == u).lower()}>"
+            reg = k == u and os.environ.get("ISAL_HIP_CRC64_SRC_CHAIN") == "reg"
+            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(reg).lower()}>"
             workload = (f"C2 encode + CRC64 (crc64_ecma_refl) of all k+p shards in one pass: k={k} "
                         f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
         elif args.workload == "crc64":

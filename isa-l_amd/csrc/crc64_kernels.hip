@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "ec_device.h"
 
@@ -405,11 +406,28 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
   }
 }
 
+// Sources per load group of the fused kernel: the largest candidate dividing
+// k (ISAL_HIP_CRC64_FUSED_U overrides it, when it divides k, for tuning).
 int group_u(int k) {
   static const int cand[] = {12, 10, 8, 6, 5, 4};
+  const char* e = getenv("ISAL_HIP_CRC64_FUSED_U");
+  if (e) {
+    const int v = atoi(e);
+    for (int u : cand)
+      if (v == u && k >= u && k % u == 0) return u;
+  }
   for (int u : cand)
     if (k >= u && k % u == 0) return u;
   return 4;
+}
+
+// Source chains in registers when the k sources form one load group only with
+// ISAL_HIP_CRC64_SRC_CHAIN=reg: on the C2 shape the register variant (209
+// VGPRs, 2 waves/SIMD) is 5 % slower than LDS chains at 3 waves/SIMD
+// (profiles/r01_encode_crc64_sweep.txt).
+bool src_chain_reg64() {
+  const char* e = getenv("ISAL_HIP_CRC64_SRC_CHAIN");
+  return e && strcmp(e, "reg") == 0;
 }
 
 template <int P, int U>
@@ -417,7 +435,7 @@ void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_
                     const uint32_t* tbl, int len, int k, unsigned nitems,
                     const isal_hip_crc64_geom& g, const uint64_t* tabs, uint64_t* part) {
   const int ragged = g.tail != 0;
-  if (k == U)
+  if (k == U && src_chain_reg64())
     hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, true>), dim3(grid), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),
                        static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), ragged, tabs, part);

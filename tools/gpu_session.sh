@@ -72,6 +72,11 @@ for s in $STEPS; do
                 run pmc_write_crc64 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_crc64" -o w -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 3 --warmup 1
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_crc64.csv" "workload=crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_crc64" "$OUT/pmc_write_crc64" crc64_shards
                 ;;
+        encrc64sweep)
+                for cfg in ${ENCRC64_CFGS:-reg:10 lds:10 lds:5}; do
+                        ISAL_HIP_CRC64_SRC_CHAIN=${cfg%:*} ISAL_HIP_CRC64_FUSED_U=${cfg#*:} run bench_encrc64_${cfg/:/_u} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
+                done
+                ;;
         decode)
                 run bench_decode 300 python bench.py --workload decode --no-cpu-baseline
                 ;;
