@@ -92,6 +92,14 @@ def test_extension_api_rejects_bad_arguments_without_gpu(engine):
     assert L.isal_hip_batch_encode(None, None) == -1
     assert L.isal_hip_batch_update(None, 0, None) == -1
     assert L.isal_hip_batch_destroy(None) == 0
+    for name in ("isal_hip_batch_crc64", "isal_hip_batch_encode_crc64"):
+        fn = getattr(L, name)
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_ulonglong, ctypes.c_void_p, ctypes.c_void_p]
+        assert fn(None, 0, 0, None, None) == -1  # no batch
+    for name in ("isal_hip_batch_encode_crc", "isal_hip_batch_crc"):
+        fn = getattr(L, name)
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+        assert fn(None, 0, None, None) == -1
     f = L.isal_hip_pipe_create
     f.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
