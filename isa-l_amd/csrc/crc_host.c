@@ -130,6 +130,25 @@ isal_hip_crc32c_tables(uint32_t *tabs)
                 }
 }
 
+/* Tables of the multi-tile chain step from the base tables: every entry of a
+ * chunk map shifted by m tiles is entry * x^(8*4096*m) mod P; Z^(4096*4) of a
+ * field value is its Z^4096 entry shifted by three more tiles. */
+void
+isal_hip_crc32c_ext_tables(const uint32_t *tabs, uint32_t *ext)
+{
+        int m, e;
+        const uint32_t z3 = isal_hip_crc32c_xpow8n(3ULL * ISAL_HIP_CRC_TILE);
+        for (m = 1; m <= 3; m++) {
+                const uint32_t zm = isal_hip_crc32c_xpow8n((unsigned long long) m * ISAL_HIP_CRC_TILE);
+                for (e = 0; e < ISAL_HIP_CRC_CHUNK_DWORDS; e++)
+                        ext[(m - 1) * ISAL_HIP_CRC_CHUNK_DWORDS + e] =
+                                isal_hip_crc32c_mulmod(tabs[ISAL_HIP_CRC_CHUNK_TAB + e], zm);
+        }
+        for (e = 0; e < ISAL_HIP_CRC_FIELDS * 32; e++)
+                ext[3 * ISAL_HIP_CRC_CHUNK_DWORDS + e] =
+                        isal_hip_crc32c_mulmod(tabs[ISAL_HIP_CRC_SHIFT_TAB + e], z3);
+}
+
 /* Geometry of the per-lane partials for shards of `len` bytes, `tt` tiles per
  * workgroup (see isal_hip_internal.h). */
 void

@@ -74,12 +74,17 @@ __device__ __forceinline__ uint32_t lookup7(const uint32_t* t, uint32_t w) {
   return xor3(xor3(at(0), at(1), at(2)), xor3(at(3), at(4), at(5)), at(6));
 }
 
+// The chunk map whose 28 field tables start at t, applied to a 16-byte chunk.
+__device__ __forceinline__ uint32_t chunk_map(const uint32_t* t, uint32_t w0, uint32_t w1,
+                                              uint32_t w2, uint32_t w3) {
+  constexpr int D = ISAL_HIP_CRC_FIELDS * 32;  // tables per dword of the chunk
+  return xor3(lookup7(t, w0), lookup7(t + D, w1), lookup7(t + 2 * D, w2)) ^ lookup7(t + 3 * D, w3);
+}
+
 // crc(0, 16 bytes): 28 conflict-free lookups.
 __device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, uint32_t w0, uint32_t w1,
                                               uint32_t w2, uint32_t w3) {
-  const uint32_t* t = lt + ISAL_HIP_CRC_CHUNK_TAB;
-  constexpr int D = ISAL_HIP_CRC_FIELDS * 32;  // tables per dword of the chunk
-  return xor3(lookup7(t, w0), lookup7(t + D, w1), lookup7(t + 2 * D, w2)) ^ lookup7(t + 3 * D, w3);
+  return chunk_map(lt + ISAL_HIP_CRC_CHUNK_TAB, w0, w1, w2, w3);
 }
 
 __device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, const uint4& x) {
@@ -118,13 +123,29 @@ __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
 // one 16-byte load in flight per lane leaves the kernel latency-bound.
 constexpr unsigned kCrcBatch = 8;
 
-template <bool VEC>
+// M > 1 advances the chain M tiles per step:
+//   a = Z^(4096*M)(a) ^ XOR_h (Z^(4096*(M-1-h)) o crc(0, .))(chunk_h)
+// with the shifted chunk maps of the EXT tables: 7 + 28*M lookups per M tiles
+// instead of 35*M.
+template <int M>
+constexpr int shards_lds_dw() {
+  return kCrcTabDw + (M > 1 ? (M - 1) * ISAL_HIP_CRC_CHUNK_DWORDS + ISAL_HIP_CRC_FIELDS * 32 : 0);
+}
+
+template <bool VEC, int M>
 __global__ __launch_bounds__(kBlock) void crc32c_shards(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int idx0, int nsh, int len,
     unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, unsigned ntiles,
     const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part, uint32_t* __restrict__ tail,
     int nshard_total, int shard0) {
-  __shared__ uint32_t lt[kCrcTabDw];
+  static_assert(kCrcBatch % M == 0, "chain step divides the load batch");
+  __shared__ uint32_t lt[shards_lds_dw<M>()];
+  if constexpr (M > 1) {
+    // chunk maps m = 1..3, then Z^(4096*4)
+    static_assert(M == 4, "EXT tables hold the step-4 shift only");
+    for (int i = threadIdx.x; i < shards_lds_dw<M>() - kCrcTabDw; i += kBlock)
+      lt[kCrcTabDw + i] = tabs[ISAL_HIP_CRC_EXT_TAB + i];
+  }
   load_crc_tables(lt, tabs);
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned si = w / nblk, blk = w - si * nblk;
@@ -153,8 +174,20 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards(
           for (unsigned g = 0; g < kCrcBatch; ++g)
             xn[g] = load16<kBufNT>(base, static_cast<long long>(t + kCrcBatch + g) * kTile + lane, len);
         }
+        if constexpr (M == 1) {
 #pragma unroll
-        for (unsigned g = 0; g < kCrcBatch; ++g) a = shift_tile(lt, a) ^ chunk_crc(lt, x[g]);
+          for (unsigned g = 0; g < kCrcBatch; ++g) a = shift_tile(lt, a) ^ chunk_crc(lt, x[g]);
+        } else {
+#pragma unroll
+          for (unsigned g = 0; g < kCrcBatch; g += M) {
+            uint32_t c = chunk_crc(lt, x[g + M - 1]);
+#pragma unroll
+            for (int h = 0; h < M - 1; ++h)
+              c ^= chunk_map(lt + kCrcTabDw + (M - 2 - h) * ISAL_HIP_CRC_CHUNK_DWORDS, x[g + h].x,
+                             x[g + h].y, x[g + h].z, x[g + h].w);
+            a = lookup7(lt + kCrcTabDw + (M - 1) * ISAL_HIP_CRC_CHUNK_DWORDS, a) ^ c;
+          }
+        }
       }
     }
     for (; t < t1; ++t) {
@@ -444,6 +477,14 @@ constexpr unsigned kMaxCrcItems = 1u << 30;
 template <int UU>
 using FusedPol = EncPol<UU, kNT, kNT>;
 
+// Tiles per chain step of crc32c_shards (ISAL_HIP_CRC_STEP = 1 or 4). Unlike
+// CRC64 the CRC32C kernel is not bound by its lookups: step 4 measured 2.90 ms
+// vs 2.87 ms per C2 step (profiles/r01_crc_step_sweep.txt), so 1 by default.
+int crc_step() {
+  const char* e = getenv("ISAL_HIP_CRC_STEP");
+  return e && atoi(e) == 4 ? 4 : 1;
+}
+
 unsigned crc_grid(unsigned long long nitems) {
   return static_cast<unsigned>(nitems);
 }
@@ -523,16 +564,18 @@ extern "C" int isal_hip_launch_crc(const uint64_t* d_ptrs, int ptr_stride, int i
     const uint64_t* ptrs = d_ptrs + s0 * ptr_stride;
     uint32_t* part = d_part + static_cast<size_t>(s0) * nshard_total * g.nblk * kBlock;
     uint32_t* tail = d_tail + static_cast<size_t>(s0) * nshard_total * kBlock;
-    if (vec16)
-      hipLaunchKernelGGL(crc32c_shards<true>, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
-                         ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
-                         static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
-                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
+#define CRC_SHARDS(V, M)                                                                    \
+  hipLaunchKernelGGL((crc32c_shards<V, M>), dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,     \
+                     ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),           \
+                     static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),                   \
+                     static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0)
+    if (!vec16)
+      CRC_SHARDS(false, 1);
+    else if (crc_step() == 4)
+      CRC_SHARDS(true, 4);
     else
-      hipLaunchKernelGGL(crc32c_shards<false>, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
-                         ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
-                         static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
-                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
+      CRC_SHARDS(true, 1);
+#undef CRC_SHARDS
     isal_hip_count_launch();
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);

@@ -98,6 +98,11 @@ void isal_hip_count_launch(void);
 #define ISAL_HIP_CRC_SHIFT_TAB (ISAL_HIP_CRC_CHUNK_TAB + 4 * ISAL_HIP_CRC_FIELDS * 32)
 #define ISAL_HIP_CRC_TAB_DWORDS (ISAL_HIP_CRC_SHIFT_TAB + ISAL_HIP_CRC_FIELDS * 32)
 #define ISAL_HIP_CRC_PLAN_DWORDS (2 * 1024 + 2 * 256 + 4)
+/* Multi-tile chain step of crc32c_shards, stored after the plan:
+ * Z^(4096*m) o crc(0, chunk) for m = 1..3, then Z^(4096*4). */
+#define ISAL_HIP_CRC_CHUNK_DWORDS (4 * ISAL_HIP_CRC_FIELDS * 32)
+#define ISAL_HIP_CRC_EXT_TAB (ISAL_HIP_CRC_TAB_DWORDS + ISAL_HIP_CRC_PLAN_DWORDS)
+#define ISAL_HIP_CRC_EXT_DWORDS (3 * ISAL_HIP_CRC_CHUNK_DWORDS + ISAL_HIP_CRC_FIELDS * 32)
 #define ISAL_HIP_CRC_MAX_FUSED_K 64 /* fused encode keeps k source partials in LDS */
 
 typedef struct {
@@ -171,6 +176,7 @@ int isal_hip_launch_encode_crc64(const uint64_t *d_ptrs, int k, int rows, long l
 uint32_t isal_hip_crc32c_mulmod(uint32_t a, uint32_t b);
 uint32_t isal_hip_crc32c_xpow8n(unsigned long long n);
 void isal_hip_crc32c_tables(uint32_t *tabs);
+void isal_hip_crc32c_ext_tables(const uint32_t *tabs, uint32_t *ext);
 void isal_hip_crc_geometry(long long len, int tt, isal_hip_crc_geom *g);
 void isal_hip_crc32c_plan(long long len, int tt, uint32_t *plan);
 

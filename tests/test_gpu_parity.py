@@ -422,6 +422,33 @@ CRC_SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("step", [1, 4])
+@pytest.mark.parametrize("k,rows,n,ns,tt", [(10, 4, 65536, 3, None), (3, 2, 4096 * 45 + 48, 2, 13),
+                                            (2, 1, 4096 * 8, 2, 8), (1, 1, 4096 * 7 + 5, 2, None)])
+def test_crc_chain_step(engine, oracle, gpu, monkeypatch, step, k, rows, n, ns, tt):
+    """crc32c_shards advancing its chain 1 or 4 tiles per step (shifted chunk
+    maps, ISAL_HIP_CRC_STEP) == oracle crc32_iscsi, incl. blocks whose tile
+    count is not a multiple of the load batch."""
+    import torch
+
+    monkeypatch.setenv("ISAL_HIP_CRC_STEP", str(step))
+    if tt:
+        monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+    a = oracle.gf_gen_rs_matrix(k + rows, k)
+    tbls = engine.ec_init_tables(k, rows, a[k * k:].copy())
+    bufs = [fill_bytes(n, 17 * s + j + step) for s in range(ns) for j in range(k + rows)]
+    store = [_dev(torch, h, gpu) for h in bufs]
+    ptr = [int(t.data_ptr()) for t in store]
+    dptr = [ptr[s * (k + rows) + j] for s in range(ns) for j in range(k)]
+    cptr = [ptr[s * (k + rows) + k + l] for s in range(ns) for l in range(rows)]
+    out = torch.zeros(ns * (k + rows), dtype=torch.int32, device=gpu)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.crc(0x1234567, out, 0)
+    torch.cuda.synchronize()
+    assert [int(v) & 0xFFFFFFFF for v in out.tolist()] == [oracle.crc32_iscsi(h, 0x1234567) for h in bufs]
+    b.close()
+
+
 @pytest.mark.parametrize("k,rows,n,ns,skew", CRC_SHAPES)
 def test_encode_crc_vs_oracle(engine, oracle, gpu, k, rows, n, ns, skew):
     """Fused encode + CRC: parity == oracle encode, every shard's CRC == oracle

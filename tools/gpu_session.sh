@@ -77,6 +77,13 @@ for s in $STEPS; do
                         ISAL_HIP_CRC64_SRC_CHAIN=${cfg%:*} ISAL_HIP_CRC64_FUSED_U=${cfg#*:} run bench_encrc64_${cfg/:/_u} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
                 done
                 ;;
+        crcstep)
+                run pytest_gpu_crc 300 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
+                for m in 1 4; do
+                        ISAL_HIP_CRC_STEP=$m run bench_crc_step$m 300 python bench.py --workload crc --no-cpu-baseline
+                done
+                run rocprof_crconly 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_crconly" -o crconly -- python3 bench.py --workload crc --no-cpu-baseline
+                ;;
         decode)
                 run bench_decode 300 python bench.py --workload decode --no-cpu-baseline
                 ;;
