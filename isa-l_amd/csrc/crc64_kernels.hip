@@ -15,6 +15,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "ec_device.h"
 
 namespace {
@@ -295,6 +297,21 @@ __device__ __forceinline__ void load_grp(uint4 (&x)[U], const uint64_t* __restri
   for (int u = 0; u < U; ++u) x[u] = load16<kNT>(sp[j + u], off, len);
 }
 
+// LDS layout of the fused kernel: chunk map, Z^4096 [kKernTab], then the chunk
+// map followed by one tile (T1) and Z^8192.
+constexpr int kT1 = kKernTab, kZ2 = kKernTab + kCE;
+
+// One chain step of phase PH (0 single, 1 even, 2 odd tile of a pair).
+template <int PH>
+__device__ __forceinline__ uint64_t chain_step(const uint64_t* lt, uint64_t a, uint32_t w0,
+                                               uint32_t w1, uint32_t w2, uint32_t w3) {
+  const uint64_t c = chunk_crc(lt + (PH == 1 ? kT1 : kChunk), w0, w1, w2, w3);
+  if constexpr (PH == 2)
+    return a ^ c;
+  else
+    return apply_op(lt + (PH == 1 ? kZ2 : kShift), a) ^ c;
+}
+
 template <int P, int U, bool REG>
 constexpr int fused64_waves() {
   constexpr int est = (4 * U * (REG ? 2 : 1) + 6 * P + (REG ? 2 * U : 0) + 88 + 7) / 8 * 8;
@@ -305,11 +322,13 @@ constexpr int fused64_waves() {
 template <int P, int U, bool REG>
 __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encode_crc64_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, const uint32_t* __restrict__ tbl, int len,
-    int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged,
+    int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged, int pair,
     const uint64_t* __restrict__ tabs, uint64_t* __restrict__ part) {
-  __shared__ uint64_t lt[kKernTab];
+  __shared__ uint64_t lt[kKernTab + kCE + kOp];
   extern __shared__ uint64_t la[];  // [k][kBlock] source chains when !REG
   load_lds<kKernTab>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
+  load_lds<kCE>(lt + kT1, tabs + ISAL_HIP_CRC64_CHUNKX_TAB);
+  load_lds<kOp>(lt + kZ2, tabs + ISAL_HIP_CRC64_SHIFTX_TAB);
   __syncthreads();
   const int nsh = k + P;
   const long long lane = threadIdx.x * kVec;
@@ -324,21 +343,38 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
     for (int j = 0; j < (REG ? U : 1); ++j) ra[j] = 0;
     if constexpr (!REG)
       for (int j = 0; j < k; ++j) la[j * kBlock + threadIdx.x] = 0;
-    auto feed = [&](int j, const uint4& x) __attribute__((always_inline)) {
-      const uint64_t c = chunk_crc(lt + kChunk, x.x, x.y, x.z, x.w);
-      if constexpr (REG) {
-        ra[j] = apply_op(lt + kShift, ra[j]) ^ c;
-      } else {
-        uint64_t* a = la + j * kBlock + threadIdx.x;
-        *a = apply_op(lt + kShift, *a) ^ c;
-      }
+    // Chain phase of a tile (uniform across the workgroup, a template
+    // argument of the tile body). With pair, tiles go in pairs: the even tile
+    // applies a = Z^8192(a) ^ T1(chunk), the odd one a ^= raw(0, chunk) — 70
+    // lookups per two tiles instead of 84, no extra state; an unpaired tile
+    // takes the single step a = Z^4096(a) ^ raw(0, chunk).
+    auto phase_of = [&](unsigned t) __attribute__((always_inline)) {
+      return !pair ? 0 : ((t - t0) & 1) ? 2 : (t + 1 < t1 ? 1 : 0);
     };
-    auto out = [&](uint32_t (&acc)[P][4], long long off) __attribute__((always_inline)) {
+    auto with_phase = [&](int ph, auto&& body) __attribute__((always_inline)) {
+      if (ph == 1)
+        body(std::integral_constant<int, 1>{});
+      else if (ph == 2)
+        body(std::integral_constant<int, 2>{});
+      else
+        body(std::integral_constant<int, 0>{});
+    };
+    auto tile_body = [&](auto phc, uint32_t (&acc)[P][4], long long off, auto&& macs)
+                         __attribute__((always_inline)) {
+      constexpr int PH = decltype(phc)::value;
+      auto feed = [&](int j, const uint4& x) __attribute__((always_inline)) {
+        if constexpr (REG) {
+          ra[j] = chain_step<PH>(lt, ra[j], x.x, x.y, x.z, x.w);
+        } else {
+          uint64_t* a = la + j * kBlock + threadIdx.x;
+          *a = chain_step<PH>(lt, *a, x.x, x.y, x.z, x.w);
+        }
+      };
+      macs(feed);
 #pragma unroll
       for (int l = 0; l < P; ++l) {
         store16<kNT>(sp[k + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
-        ao[l] = apply_op(lt + kShift, ao[l]) ^
-                chunk_crc(lt + kChunk, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+        ao[l] = chain_step<PH>(lt, ao[l], acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
       }
     };
     if constexpr (REG) {
@@ -355,8 +391,11 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
         uint32_t acc[P][4] = {};
         int z = 0;  // opaque zero: keeps the coefficient loads inside the loop
         asm volatile("" : "+s"(z));
-        mac_feed<P, U>(acc, x, 0, tbl + z, feed);
-        out(acc, off);
+        with_phase(phase_of(t), [&](auto phc) __attribute__((always_inline)) {
+          tile_body(phc, acc, off, [&](auto& feed) __attribute__((always_inline)) {
+            mac_feed<P, U>(acc, x, 0, tbl + z, feed);
+          });
+        });
       }
     } else {
       for (unsigned t = t0; t < t1; ++t) {
@@ -364,18 +403,21 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
         uint32_t acc[P][4] = {};
         int z = 0;
         asm volatile("" : "+s"(z));
-        int j = 0;
-        for (; j + U <= k; j += U) {
-          uint4 x[U];
-          load_grp<U>(x, sp, j, off, len);
-          mac_feed<P, U>(acc, x, j, tbl + z, feed);
-        }
-        for (; j < k; ++j) {
-          uint4 x[1];
-          load_grp<1>(x, sp, j, off, len);
-          mac_feed<P, 1>(acc, x, j, tbl + z, feed);
-        }
-        out(acc, off);
+        with_phase(phase_of(t), [&](auto phc) __attribute__((always_inline)) {
+          tile_body(phc, acc, off, [&](auto& feed) __attribute__((always_inline)) {
+            int j = 0;
+            for (; j + U <= k; j += U) {
+              uint4 x[U];
+              load_grp<U>(x, sp, j, off, len);
+              mac_feed<P, U>(acc, x, j, tbl + z, feed);
+            }
+            for (; j < k; ++j) {
+              uint4 x[1];
+              load_grp<1>(x, sp, j, off, len);
+              mac_feed<P, 1>(acc, x, j, tbl + z, feed);
+            }
+          });
+        });
       }
     }
     if (ragged && blk + 1 == nblk) {  // encode the tail tile; combine checksums it
@@ -421,6 +463,12 @@ int group_u(int k) {
   return 4;
 }
 
+// Paired chain steps in the fused kernel (ISAL_HIP_CRC64_FUSED_PAIR=0: off).
+int pair_step() {
+  const char* e = getenv("ISAL_HIP_CRC64_FUSED_PAIR");
+  return !(e && atoi(e) == 0);
+}
+
 // Source chains in registers when the k sources form one load group only with
 // ISAL_HIP_CRC64_SRC_CHAIN=reg: on the C2 shape the register variant (209
 // VGPRs, 2 waves/SIMD) is 5 % slower than LDS chains at 3 waves/SIMD
@@ -438,12 +486,13 @@ void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_
   if (k == U && src_chain_reg64())
     hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, true>), dim3(grid), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),
-                       static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), ragged, tabs, part);
+                       static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), ragged, pair_step(),
+                       tabs, part);
   else
     hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, false>), dim3(grid), dim3(kBlock),
                        static_cast<size_t>(k) * kBlock * 8, s, ptrs, ptr_stride, tbl, len, k, nitems,
                        static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
-                       static_cast<unsigned>(g.nfull), ragged, tabs, part);
+                       static_cast<unsigned>(g.nfull), ragged, pair_step(), tabs, part);
 }
 
 template <int P>

@@ -676,6 +676,18 @@ def test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns
     b.close()
 
 
+@pytest.mark.parametrize("pair,chain", [(0, "lds"), (1, "reg"), (0, "reg")])
+@pytest.mark.parametrize("k,rows,n,ns,skew,tt,variant", ENCODE_CRC64_SHAPES[:5])
+def test_encode_crc64_knobs(engine, oracle, gpu, monkeypatch, pair, chain, k, rows, n, ns, skew, tt,
+                            variant):
+    """The fused encode + CRC64 kernel with unpaired chain steps
+    (ISAL_HIP_CRC64_FUSED_PAIR=0) and with register source chains
+    (ISAL_HIP_CRC64_SRC_CHAIN=reg) == oracle as the defaults are."""
+    monkeypatch.setenv("ISAL_HIP_CRC64_FUSED_PAIR", str(pair))
+    monkeypatch.setenv("ISAL_HIP_CRC64_SRC_CHAIN", chain)
+    test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant)
+
+
 def test_encode_crc64_c2_full_size(engine, oracle, gpu):
     """C2 at full size through the fused encode + CRC64 pass: parity identical
     to the plain encode kernel's, CRC64s == the standalone CRC64 pass on all
