@@ -42,7 +42,9 @@ int isal_hip_batch_create(isal_hip_batch **out, int len, int k, int rows,
                           const unsigned char *gftbls, int nstripes, unsigned char *const *data,
                           unsigned char *const *coding);
 
-/* Replace the coefficient tables (e.g. a decode matrix) of an existing batch. */
+/* Replace the coefficient tables (e.g. a decode matrix) of an existing batch.
+ * Synchronises the device first: launches already queued on any stream keep
+ * the coefficients they were enqueued with. */
 int isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls);
 
 /* Enqueue ec_encode_data for every stripe of the batch on stream. */
@@ -80,8 +82,8 @@ int isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, 
  * memory, = crc64_<variant>(init, shard, len) with the reference's semantics
  * (include/crc64.h:54-163, crc/crc64_base.c:569-670: register starts at ~init,
  * inverted on return; refl / norm bit order). Variants in the order of
- * crc64.h. The first call per variant uploads its tables (and synchronises
- * the device when it replaces another variant's); partials take
+ * crc64.h. The first call per variant uploads its own tables (~80 KiB, kept
+ * for the batch's lifetime; no device synchronisation); partials take
  * nstripes*(k+rows) * ceil(len/65536) * 2 KiB of device memory.
  */
 #define ISAL_HIP_CRC64_ECMA_REFL 0
@@ -132,6 +134,31 @@ int isal_hip_pipe_submit(isal_hip_pipe *p, unsigned char *const *data, unsigned 
 int isal_hip_pipe_flush(isal_hip_pipe *p);
 
 int isal_hip_pipe_destroy(isal_hip_pipe *p);
+
+/* ---- routing of the drop-in calls and configuration --------------------- */
+
+/*
+ * The synchronous drop-in calls (erasure_code.h, gf_vect_mul.h, raid.h) route
+ * each call by where its shards live and how large it is:
+ *   - any device-resident shard: the GPU kernels;
+ *   - host-resident shards, (k + rows) * len > ISAL_HIP_CPU_MAX_BYTES: the GPU
+ *     kernels through pinned / HBM staging;
+ *   - host-resident shards up to ISAL_HIP_CPU_MAX_BYTES (default 1 MiB), or a
+ *     host without a usable GPU: the engine's CPU route.
+ * ISAL_HIP_BACKEND=gpu forces the kernels for every call (and aborts when no
+ * GPU is usable), =cpu sends every host-resident call to the CPU route,
+ * =auto (default) is the rule above. If a HIP call fails during a
+ * host-resident call, the call completes on the CPU route and the failure is
+ * reported once on stderr; ISAL_HIP_LOG=1 logs every call's route.
+ * Environment knobs are read once; isal_hip_config_reload() re-reads them
+ * (call it only while no other thread is inside the library).
+ */
+void isal_hip_config_reload(void);
+
+/* Drop-in calls served by the CPU route, and of those the HIP-failure
+ * fallbacks, since the process started. */
+unsigned long long isal_hip_cpu_calls(void);
+unsigned long long isal_hip_fallbacks(void);
 
 /* ---- introspection (tests, benchmarks) --------------------------------- */
 

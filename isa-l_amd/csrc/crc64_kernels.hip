@@ -243,15 +243,13 @@ constexpr unsigned long long kMaxItems = 1ull << 30;
 // Measured on the C2 shape (profiles/r01_crc64_step_sweep.txt): 2 tiles per
 // step with 4 loads in flight is fastest; 4 per step costs occupancy (LDS).
 int chain_step() {
-  const char* e = getenv("ISAL_HIP_CRC64_STEP");
-  const int v = e ? atoi(e) : 2;
-  return v == 1 || v == 4 ? v : 2;
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_STEP);
+  return v == 1 || v == 4 ? static_cast<int>(v) : 2;
 }
 
 // Full tiles loaded per batch (ISAL_HIP_CRC64_BATCH = 4 or 8).
 int load_batch() {
-  const char* e = getenv("ISAL_HIP_CRC64_BATCH");
-  return e && atoi(e) == 8 ? 8 : 4;
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_BATCH) == 8 ? 8 : 4;
 }
 
 // ---------------------------------------------------------------------------
@@ -452,9 +450,8 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
 // k (ISAL_HIP_CRC64_FUSED_U overrides it, when it divides k, for tuning).
 int group_u(int k) {
   static const int cand[] = {12, 10, 8, 6, 5, 4};
-  const char* e = getenv("ISAL_HIP_CRC64_FUSED_U");
-  if (e) {
-    const int v = atoi(e);
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_FUSED_U);
+  if (v > 0) {
     for (int u : cand)
       if (v == u && k >= u && k % u == 0) return u;
   }
@@ -465,8 +462,7 @@ int group_u(int k) {
 
 // Paired chain steps in the fused kernel (ISAL_HIP_CRC64_FUSED_PAIR=0: off).
 int pair_step() {
-  const char* e = getenv("ISAL_HIP_CRC64_FUSED_PAIR");
-  return !(e && atoi(e) == 0);
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_FUSED_PAIR) != 0;
 }
 
 // Source chains in registers when the k sources form one load group only with
@@ -474,8 +470,7 @@ int pair_step() {
 // VGPRs, 2 waves/SIMD) is 5 % slower than LDS chains at 3 waves/SIMD
 // (profiles/r01_encode_crc64_sweep.txt).
 bool src_chain_reg64() {
-  const char* e = getenv("ISAL_HIP_CRC64_SRC_CHAIN");
-  return e && strcmp(e, "reg") == 0;
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_SRC_CHAIN) == 1;  // "reg"
 }
 
 template <int P, int U>

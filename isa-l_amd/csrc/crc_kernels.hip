@@ -481,8 +481,7 @@ using FusedPol = EncPol<UU, kNT, kNT>;
 // CRC64 the CRC32C kernel is not bound by its lookups: step 4 measured 2.90 ms
 // vs 2.87 ms per C2 step (profiles/r01_crc_step_sweep.txt), so 1 by default.
 int crc_step() {
-  const char* e = getenv("ISAL_HIP_CRC_STEP");
-  return e && atoi(e) == 4 ? 4 : 1;
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC_STEP) == 4 ? 4 : 1;
 }
 
 unsigned crc_grid(unsigned long long nitems) {
@@ -499,11 +498,7 @@ int enc_group_crc(int k) {
 // ISAL_HIP_CRC_SRC_CHAIN=lds keeps the source chains in LDS even when the k
 // sources form one load group (tuning knob; default: registers).
 bool src_chain_reg() {
-  static const bool reg = [] {
-    const char* e = getenv("ISAL_HIP_CRC_SRC_CHAIN");
-    return !(e && strcmp(e, "lds") == 0);
-  }();
-  return reg;
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC_SRC_CHAIN) != 0;  // not "lds"
 }
 
 template <int P, int U>

@@ -213,11 +213,8 @@ __global__ __launch_bounds__(kBlock) void ec_update_b1(const uint64_t* __restric
 constexpr unsigned kMaxItems = 1u << 30;  // keep w / tiles in 32-bit scalar math
 
 unsigned grid_cap() {
-  static unsigned cap = [] {
-    const char* e = getenv("ISAL_HIP_GRID_CAP");
-    return e ? static_cast<unsigned>(strtoul(e, nullptr, 10)) : 0u;
-  }();
-  return cap;
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_GRID_CAP);
+  return v > 0 ? static_cast<unsigned>(v) : 0u;
 }
 
 unsigned grid_for(unsigned nitems) {

@@ -74,6 +74,35 @@ unsigned long long isal_hip_run(int op, int len, int k, int rows, int vec_i,
 /* Launch counter shared by the shim and the launchers. */
 void isal_hip_count_launch(void);
 
+/* ---- environment knobs (isal_hip_knobs.c): read once, -1 when unset ------- */
+enum {
+        ISAL_HIP_KNOB_BACKEND,       /* auto(0) | gpu(1) | cpu(2); -2 = unknown word */
+        ISAL_HIP_KNOB_CPU_MAX_BYTES, /* auto route: host calls up to this many bytes run on the CPU */
+        ISAL_HIP_KNOB_LOG,           /* 1: log every drop-in call's route to stderr */
+        ISAL_HIP_KNOB_CPU_SIMD,      /* 0: CPU route without AVX2 (per-byte; tests) */
+        ISAL_HIP_KNOB_STAGE_MB,
+        ISAL_HIP_KNOB_GRID_CAP,
+        ISAL_HIP_KNOB_CRC_TILES,
+        ISAL_HIP_KNOB_CRC_STEP,
+        ISAL_HIP_KNOB_CRC_SRC_CHAIN, /* lds(0) | reg(1) */
+        ISAL_HIP_KNOB_CRC64_STEP,
+        ISAL_HIP_KNOB_CRC64_BATCH,
+        ISAL_HIP_KNOB_CRC64_FUSED_U,
+        ISAL_HIP_KNOB_CRC64_FUSED_PAIR,
+        ISAL_HIP_KNOB_CRC64_SRC_CHAIN, /* lds(0) | reg(1) */
+        ISAL_HIP_KNOB_COUNT
+};
+long long isal_hip_knob(int id);
+
+/* ---- the host (CPU) route (ec_cpu.c) ---------------------------------------
+ * Same ops and return value as isal_hip_run, over HOST-resident shards only,
+ * for columns [c0, len): the drop-in calls' route for small host calls, for
+ * ISAL_HIP_BACKEND=cpu, for hosts without a GPU, and the fallback when a HIP
+ * call fails mid-way (columns before c0 are already final). */
+unsigned long long isal_cpu_run(int op, long long c0, int len, int k, int rows, int vec_i,
+                                const unsigned char *gftbls, unsigned char *const *src, int nsrc,
+                                unsigned char *const *dst);
+
 /* ---- CRC32C of shards (crc_host.c, crc_kernels.hip) -------------------------
  * crc32_iscsi semantics (reference crc/crc_base.c:205-219). Each workgroup
  * covers `tt` consecutive 4 KiB tiles of one shard; lane L owns bytes

@@ -1,0 +1,81 @@
+/*
+ * isal_hip_knobs.c — the engine's ISAL_HIP_* environment knobs.
+ *
+ * Every knob is read from the environment ONCE (first use) into a table, so
+ * no launch or drop-in call pays a getenv; isal_hip_config_reload() re-reads
+ * them (tests and tuning sweeps change knobs inside one process). The
+ * reference has no runtime configuration beyond its CPU dispatch (SURVEY.md
+ * §5 "Config / flags"); these knobs are the engine's own.
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "isal_hip.h"
+#include "isal_hip_internal.h"
+
+typedef struct {
+        const char *name;
+        /* string-valued knobs map their words to ints; NULL = integer knob */
+        const char *const *words;
+} knob_def;
+
+static const char *const backend_words[] = {"auto", "gpu", "cpu", NULL};
+static const char *const chain_words[] = {"lds", "reg", NULL};
+
+static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
+        [ISAL_HIP_KNOB_BACKEND] = {"ISAL_HIP_BACKEND", backend_words},
+        [ISAL_HIP_KNOB_CPU_MAX_BYTES] = {"ISAL_HIP_CPU_MAX_BYTES", NULL},
+        [ISAL_HIP_KNOB_LOG] = {"ISAL_HIP_LOG", NULL},
+        [ISAL_HIP_KNOB_CPU_SIMD] = {"ISAL_HIP_CPU_SIMD", NULL},
+        [ISAL_HIP_KNOB_STAGE_MB] = {"ISAL_HIP_STAGE_MB", NULL},
+        [ISAL_HIP_KNOB_GRID_CAP] = {"ISAL_HIP_GRID_CAP", NULL},
+        [ISAL_HIP_KNOB_CRC_TILES] = {"ISAL_HIP_CRC_TILES", NULL},
+        [ISAL_HIP_KNOB_CRC_STEP] = {"ISAL_HIP_CRC_STEP", NULL},
+        [ISAL_HIP_KNOB_CRC_SRC_CHAIN] = {"ISAL_HIP_CRC_SRC_CHAIN", chain_words},
+        [ISAL_HIP_KNOB_CRC64_STEP] = {"ISAL_HIP_CRC64_STEP", NULL},
+        [ISAL_HIP_KNOB_CRC64_BATCH] = {"ISAL_HIP_CRC64_BATCH", NULL},
+        [ISAL_HIP_KNOB_CRC64_FUSED_U] = {"ISAL_HIP_CRC64_FUSED_U", NULL},
+        [ISAL_HIP_KNOB_CRC64_FUSED_PAIR] = {"ISAL_HIP_CRC64_FUSED_PAIR", NULL},
+        [ISAL_HIP_KNOB_CRC64_SRC_CHAIN] = {"ISAL_HIP_CRC64_SRC_CHAIN", chain_words},
+};
+
+static long long values[ISAL_HIP_KNOB_COUNT];
+static pthread_once_t once = PTHREAD_ONCE_INIT;
+
+static long long
+parse(const knob_def *d)
+{
+        const char *e = getenv(d->name);
+        int i;
+        if (!e || !*e)
+                return -1;
+        if (!d->words)
+                return strtoll(e, NULL, 10);
+        for (i = 0; d->words[i]; i++)
+                if (strcmp(e, d->words[i]) == 0)
+                        return i;
+        return -2; /* set, but not a known word */
+}
+
+static void
+load(void)
+{
+        int i;
+        for (i = 0; i < ISAL_HIP_KNOB_COUNT; i++)
+                values[i] = parse(&defs[i]);
+}
+
+long long
+isal_hip_knob(int id)
+{
+        pthread_once(&once, load);
+        return id >= 0 && id < ISAL_HIP_KNOB_COUNT ? values[id] : -1;
+}
+
+void
+isal_hip_config_reload(void)
+{
+        pthread_once(&once, load);
+        load();
+}

@@ -5,23 +5,29 @@
  * ec_encode_data, ec_encode_data_update, gf_vect_dot_prod, gf_vect_mad,
  * gf_vect_mul and their *_base twins) and the batched extension (isal_hip.h).
  * Replaces the reference's L2 dispatch + L3 glue (ec_multibinary.asm:79-93,
- * ec_highlevel_func.c:159-698): instead of picking a CPU ISA, every call is
- * routed to the GPU kernels in ec_kernels.hip.
+ * ec_highlevel_func.c:159-698): instead of picking a CPU ISA, calls are
+ * routed to the GPU kernels in ec_kernels.hip (small host-resident calls: the
+ * CPU route, ec_cpu.c).
  *
- * Per call:
+ * Per call (run_ec):
  *   1. classify every shard pointer (device/managed vs host) with
  *      hipPointerGetAttributes;
- *   2. stage host-resident shards through a per-thread HBM scratch buffer,
- *      in column chunks (so any len fits);
- *   3. upload the stripe's pointer table + derived coefficient tables
- *      (isal_hip_internal.h layout) from a per-thread pinned buffer;
- *   4. launch, copy host-resident outputs back, synchronise — the reference
- *      API is synchronous and results must be visible on return.
+ *   2. route: host-resident calls of at most ISAL_HIP_CPU_MAX_BYTES run on the
+ *      CPU route (ec_cpu.c) — the GPU round trip costs more than the work, as
+ *      the reference's own short-length fallback recognises
+ *      (ec_highlevel_func.c:159-194); ISAL_HIP_BACKEND=gpu|cpu|auto overrides;
+ *   3. otherwise stage host-resident shards through a per-thread pinned or HBM
+ *      buffer (zero-copy / packed / column-chunked), upload the pointer table +
+ *      derived coefficient tables, launch, copy host-resident outputs back and
+ *      synchronise — the reference API is synchronous.
  *
- * There is no CPU compute path: a HIP failure prints the failing call and
- * aborts (the reference API has no error return to carry it).
+ * Failures: the reference API has no error return, so a host-resident call
+ * must not fail where the reference would succeed. A failing HIP call hands
+ * the columns that are not yet final to the CPU route (reported once on
+ * stderr). Only a call with device-resident shards — which no CPU route can
+ * serve — or one made under ISAL_HIP_BACKEND=gpu aborts.
  * Thread safety: all mutable state is per thread (pthread key) except the
- * atomic launch counter.
+ * atomic counters and the read-once knobs.
  */
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
@@ -34,24 +40,19 @@
 #include "isal_hip.h"
 #include "isal_hip_internal.h"
 
-/* ---- errors ------------------------------------------------------------- */
+/* ---- errors, counters, routing log -------------------------------------- */
 
 static void
 die(const char *what, hipError_t e)
 {
-        fprintf(stderr, "isal_hip: %s failed: %s (%d); no CPU fallback exists, aborting\n", what,
-                hipGetErrorString(e), (int) e);
+        fprintf(stderr,
+                "isal_hip: %s failed: %s (%d) on a call with device-resident shards (or with "
+                "ISAL_HIP_BACKEND=gpu); no CPU route can serve it, aborting\n",
+                what, hipGetErrorString(e), (int) e);
         abort();
 }
 
-#define HIP_OR_DIE(call)                                                                           \
-        do {                                                                                       \
-                hipError_t e_ = (call);                                                            \
-                if (e_ != hipSuccess)                                                              \
-                        die(#call, e_);                                                            \
-        } while (0)
-
-static unsigned long long g_launches;
+static unsigned long long g_launches, g_cpu_calls, g_fallbacks;
 
 void
 isal_hip_count_launch(void)
@@ -65,6 +66,18 @@ isal_hip_kernel_launches(void)
         return __atomic_load_n(&g_launches, __ATOMIC_RELAXED);
 }
 
+unsigned long long
+isal_hip_cpu_calls(void)
+{
+        return __atomic_load_n(&g_cpu_calls, __ATOMIC_RELAXED);
+}
+
+unsigned long long
+isal_hip_fallbacks(void)
+{
+        return __atomic_load_n(&g_fallbacks, __ATOMIC_RELAXED);
+}
+
 int
 isal_hip_max_rows_per_pass(void)
 {
@@ -75,6 +88,78 @@ const char *
 isal_hip_target(void)
 {
         return "gfx950";
+}
+
+static const char *const op_names[] = {"encode", "update", "verify"};
+
+/* ISAL_HIP_LOG=1: one stderr line per drop-in call naming the route taken. */
+static void
+route_log(int op, int len, int k, int rows, const char *route, const char *why)
+{
+        if (isal_hip_knob(ISAL_HIP_KNOB_LOG) > 0)
+                fprintf(stderr, "isal_hip: %s len=%d k=%d rows=%d -> %s (%s)\n", op_names[op], len,
+                        k, rows, route, why);
+}
+
+/* A HIP failure under a host-resident call: reported once per process (every
+ * time with ISAL_HIP_LOG=1), then the call finishes on the CPU route. */
+static void
+report_fallback(const char *what, hipError_t e)
+{
+        static int reported;
+        __atomic_add_fetch(&g_fallbacks, 1ull, __ATOMIC_RELAXED);
+        if (!__atomic_exchange_n(&reported, 1, __ATOMIC_RELAXED) ||
+            isal_hip_knob(ISAL_HIP_KNOB_LOG) > 0)
+                fprintf(stderr,
+                        "isal_hip: %s failed: %s (%d); host-resident calls fall back to the CPU "
+                        "route (reported once; ISAL_HIP_LOG=1 reports each)\n",
+                        what, hipGetErrorString(e), (int) e);
+}
+
+enum { BACKEND_AUTO = 0, BACKEND_GPU = 1, BACKEND_CPU = 2 };
+
+static int
+backend(void)
+{
+        const long long v = isal_hip_knob(ISAL_HIP_KNOB_BACKEND);
+        static int warned;
+        if (v == -2 && !__atomic_exchange_n(&warned, 1, __ATOMIC_RELAXED))
+                fprintf(stderr, "isal_hip: ISAL_HIP_BACKEND must be auto, gpu or cpu; using auto\n");
+        return v == BACKEND_GPU || v == BACKEND_CPU ? (int) v : BACKEND_AUTO;
+}
+
+/* Host calls of at most this many shard bytes ((k + rows) * len) take the CPU
+ * route under ISAL_HIP_BACKEND=auto (override: ISAL_HIP_CPU_MAX_BYTES). Below
+ * it the ~30 us GPU round trip costs more than the arithmetic (DESIGN.md §3,
+ * measured crossover in profiles/r02_route_crossover.txt). */
+#define DEFAULT_CPU_MAX_BYTES ((size_t) 1 << 20)
+
+static size_t
+cpu_max_bytes(void)
+{
+        const long long v = isal_hip_knob(ISAL_HIP_KNOB_CPU_MAX_BYTES);
+        return v >= 0 ? (size_t) v : DEFAULT_CPU_MAX_BYTES;
+}
+
+/* Is a GPU usable at all? (Asked once: a host without one, or without a
+ * working driver, serves every host-resident call on the CPU route.) */
+static int gpu_ok;
+static pthread_once_t gpu_once = PTHREAD_ONCE_INIT;
+
+static void
+gpu_probe(void)
+{
+        int n = 0;
+        gpu_ok = hipGetDeviceCount(&n) == hipSuccess && n > 0;
+        if (!gpu_ok)
+                (void) hipGetLastError();
+}
+
+static int
+gpu_present(void)
+{
+        pthread_once(&gpu_once, gpu_probe);
+        return gpu_ok;
 }
 
 /* ---- per-thread context ------------------------------------------------- */
@@ -124,16 +209,21 @@ ctx_key_init(void)
         }
 }
 
+/* The calling thread's context on the current device, or NULL with *err set. */
 static ctx_t *
-ctx_get(void)
+ctx_get(hipError_t *err, const char **what)
 {
         ctx_t *c;
         int dev;
         pthread_once(&ctx_once, ctx_key_init);
-        HIP_OR_DIE(hipGetDevice(&dev));
+        if ((*err = hipGetDevice(&dev)) != hipSuccess) {
+                *what = "hipGetDevice";
+                return NULL;
+        }
         c = (ctx_t *) pthread_getspecific(ctx_key);
         if (c && c->device != dev) {
                 ctx_release(c);
+                pthread_setspecific(ctx_key, NULL);
                 c = NULL;
         }
         if (!c) {
@@ -143,57 +233,73 @@ ctx_get(void)
                         abort();
                 }
                 c->device = dev;
-                HIP_OR_DIE(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+                /* A BLOCKING stream: it is ordered after work already queued on the
+                 * legacy default stream (e.g. torch kernels that just wrote the
+                 * shards), as the synchronous reference API implies. */
+                if ((*err = hipStreamCreate(&c->stream)) != hipSuccess) {
+                        *what = "hipStreamCreate";
+                        free(c);
+                        return NULL;
+                }
                 pthread_setspecific(ctx_key, c);
         }
         return c;
 }
 
-static void
+static hipError_t
 ensure_args(ctx_t *c, size_t bytes)
 {
         size_t cap;
+        hipError_t e;
         if (bytes <= c->args_cap)
-                return;
+                return hipSuccess;
         cap = c->args_cap ? c->args_cap : 64 * 1024;
         while (cap < bytes)
                 cap *= 2;
         if (c->d_args)
-                HIP_OR_DIE(hipFree(c->d_args));
+                (void) hipFree(c->d_args);
         if (c->h_args)
-                HIP_OR_DIE(hipHostFree(c->h_args));
+                (void) hipHostFree(c->h_args);
         c->d_args = c->h_args = c->h_args_dev = NULL;
-        HIP_OR_DIE(hipMalloc(&c->d_args, cap));
+        c->args_cap = 0;
+        if ((e = hipMalloc(&c->d_args, cap)) != hipSuccess)
+                return e;
         /* coherent: kernels of the zero-copy path read arguments and shards the
          * host just wrote, and the host reads what they wrote, with no cached
          * copies in between */
-        HIP_OR_DIE(hipHostMalloc(&c->h_args, cap, hipHostMallocCoherent));
-        HIP_OR_DIE(hipHostGetDevicePointer(&c->h_args_dev, c->h_args, 0));
+        if ((e = hipHostMalloc(&c->h_args, cap, hipHostMallocCoherent)) != hipSuccess ||
+            (e = hipHostGetDevicePointer(&c->h_args_dev, c->h_args, 0)) != hipSuccess) {
+                (void) hipFree(c->d_args);
+                if (c->h_args)
+                        (void) hipHostFree(c->h_args);
+                c->d_args = c->h_args = c->h_args_dev = NULL;
+                return e;
+        }
         c->args_cap = cap;
+        return hipSuccess;
 }
 
-static void
+static hipError_t
 ensure_stage(ctx_t *c, size_t bytes)
 {
+        hipError_t e;
         if (bytes <= c->stage_cap)
-                return;
+                return hipSuccess;
         if (c->d_stage)
-                HIP_OR_DIE(hipFree(c->d_stage));
+                (void) hipFree(c->d_stage);
         c->d_stage = NULL;
-        HIP_OR_DIE(hipMalloc((void **) &c->d_stage, bytes));
+        c->stage_cap = 0;
+        if ((e = hipMalloc((void **) &c->d_stage, bytes)) != hipSuccess)
+                return e;
         c->stage_cap = bytes;
+        return hipSuccess;
 }
 
 static size_t
 stage_limit(void)
 {
-        static size_t lim;
-        if (!lim) {
-                const char *e = getenv("ISAL_HIP_STAGE_MB");
-                size_t v = e ? (size_t) strtoull(e, NULL, 10) << 20 : 0;
-                lim = v ? v : DEFAULT_STAGE_BYTES;
-        }
-        return lim;
+        const long long v = isal_hip_knob(ISAL_HIP_KNOB_STAGE_MB);
+        return v > 0 ? (size_t) v << 20 : DEFAULT_STAGE_BYTES;
 }
 
 /* ---- pointer classification ------------------------------------------- */
@@ -219,15 +325,19 @@ on_device(const void *p)
 enum { OP_ENCODE = ISAL_HIP_OP_ENCODE, OP_UPDATE = ISAL_HIP_OP_UPDATE, OP_VERIFY = ISAL_HIP_OP_VERIFY };
 
 /*
- * Three ways to run one synchronous call, by size:
+ * Routes of one synchronous call:
+ *   cpu        every shard host-resident and (k + rows) * len <= cpu_max_bytes
+ *              (ISAL_HIP_BACKEND=auto), or ISAL_HIP_BACKEND=cpu, or no GPU:
+ *              ec_cpu.c, no HIP call at all;
  *   zero-copy  len * (k + rows) <= ZC_BYTES: pointer table, coefficient tables,
  *              host-resident shards and verify slots all live in the pinned
  *              buffer and the kernel reads/writes them over PCIe — the call is
  *              one launch and one stream sync;
  *   packed     host-staged bytes <= PACK_BYTES: the same layout, moved with one
  *              H2D and one D2H DMA into/out of HBM;
- *   chunked    larger: shards staged per column chunk (run_ec below).
- * The reference's own tests make ~10^5-10^7 calls of a few KiB each.
+ *   chunked    larger: shards staged per column chunk (gpu_chunked below).
+ * A HIP failure in a host-resident call hands the columns not yet final to the
+ * CPU route; with any device-resident shard (or ISAL_HIP_BACKEND=gpu) it aborts.
  */
 #define ZC_BYTES ((size_t) 256 << 10)
 #define PACK_BYTES ((size_t) 4 << 20)
@@ -263,43 +373,64 @@ min_slot(const unsigned long long *slots, int n)
 }
 
 /* Enqueue one chunk's kernel(s) with the argument block at `args` (device or
- * zero-copy view). For OP_VERIFY returns the number of slots written at
- * args + L->slots_off. */
-static int
+ * zero-copy view). For OP_VERIFY *nslots receives the number of slots written
+ * at args + L->slots_off. */
+static hipError_t
 launch_op(ctx_t *c, int op, char *args, const layout_t *L, int nptr, int nsrc, int clen,
-          long long c0, int k, int rows, int vec_i, int vec16)
+          long long c0, int k, int rows, int vec_i, int vec16, int *nslots)
 {
         const uint64_t *ptrs = (const uint64_t *) args;
         const uint32_t *tbl = (const uint32_t *) (args + L->ptr_bytes);
-        int err, nslots = 0;
+        *nslots = 0;
         if (op == OP_VERIFY)
-                err = isal_hip_launch_verify(ptrs, nptr, 0, nsrc, tbl, clen, k, rows, c0,
-                                             (unsigned long long *) (args + L->slots_off), &nslots,
-                                             vec16, c->stream);
-        else if (op == OP_ENCODE)
-                err = isal_hip_launch_encode(ptrs, nptr, 0, nsrc, tbl, clen, k, rows, 1, vec16,
-                                             c->stream);
-        else
-                err = isal_hip_launch_update(ptrs, nptr, 0, nsrc, tbl, clen, k, rows, vec_i, 1,
-                                             vec16, c->stream);
-        if (err)
-                die("kernel launch", (hipError_t) err);
-        return nslots;
+                return (hipError_t) isal_hip_launch_verify(
+                        ptrs, nptr, 0, nsrc, tbl, clen, k, rows, c0,
+                        (unsigned long long *) (args + L->slots_off), nslots, vec16, c->stream);
+        if (op == OP_ENCODE)
+                return (hipError_t) isal_hip_launch_encode(ptrs, nptr, 0, nsrc, tbl, clen, k, rows,
+                                                           1, vec16, c->stream);
+        return (hipError_t) isal_hip_launch_update(ptrs, nptr, 0, nsrc, tbl, clen, k, rows, vec_i,
+                                                   1, vec16, c->stream);
 }
 
-/* zero-copy and packed modes (whole shards, one chunk) */
-static unsigned long long
-run_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+/* Outcome of a GPU attempt: on failure `what`/`err` name the HIP call and
+ * columns [0, done) are final, so a fallback redoes only [done, len). An
+ * update (read-modify-write) that failed while copying a chunk's parity back
+ * also reports how many output rows of [done, chunk_end) had their copy
+ * enqueued (rows_out): those must not be folded twice. */
+typedef struct {
+        hipError_t err;
+        const char *what;
+        long long done, chunk_end;
+        int rows_out;
+        unsigned long long first_bad;
+} gpu_res;
+
+#define GPU_TRY(r, call)                                                                           \
+        do {                                                                                       \
+                hipError_t e_ = (call);                                                            \
+                if (e_ != hipSuccess) {                                                            \
+                        (r).err = e_;                                                              \
+                        (r).what = #call;                                                          \
+                        return (r);                                                                \
+                }                                                                                  \
+        } while (0)
+
+/* zero-copy and packed modes (whole shards, one chunk). Host outputs are
+ * written only after the stream completed, so a failure leaves them untouched. */
+static gpu_res
+gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
           unsigned char *const *src, int nsrc, unsigned char *const *dst, const int *flag,
           int nstage, int zero_copy)
 {
+        gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         int nptr = nsrc + rows, i, s, first_out = -1, vec16 = 1, nslots;
         layout_t L = call_layout(op, len, k, rows, nptr, nstage);
         char *h, *dv;
         size_t upload;
         uint64_t *h_ptrs;
 
-        ensure_args(c, L.total);
+        GPU_TRY(r, ensure_args(c, L.total));
         h = (char *) c->h_args;
         dv = zero_copy ? (char *) c->h_args_dev : (char *) c->d_args; /* what kernels see */
         h_ptrs = (uint64_t *) h;
@@ -325,83 +456,48 @@ run_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
                         vec16 = 0;
         }
         if (!zero_copy)
-                HIP_OR_DIE(hipMemcpyAsync(c->d_args, h, upload, hipMemcpyHostToDevice, c->stream));
-        nslots = launch_op(c, op, dv, &L, nptr, nsrc, len, 0, k, rows, vec_i, vec16);
+                GPU_TRY(r, hipMemcpyAsync(c->d_args, h, upload, hipMemcpyHostToDevice, c->stream));
+        GPU_TRY(r, launch_op(c, op, dv, &L, nptr, nsrc, len, 0, k, rows, vec_i, vec16, &nslots));
         if (!zero_copy) {
                 if (op == OP_VERIFY)
-                        HIP_OR_DIE(hipMemcpyAsync(h + L.slots_off, (char *) c->d_args + L.slots_off,
+                        GPU_TRY(r, hipMemcpyAsync(h + L.slots_off, (char *) c->d_args + L.slots_off,
                                                   (size_t) nslots * 8, hipMemcpyDeviceToHost,
                                                   c->stream));
                 else if (first_out >= 0)
-                        HIP_OR_DIE(hipMemcpyAsync(h + L.stage_off + (size_t) first_out * L.slot,
+                        GPU_TRY(r, hipMemcpyAsync(h + L.stage_off + (size_t) first_out * L.slot,
                                                   (char *) c->d_args + L.stage_off +
                                                           (size_t) first_out * L.slot,
                                                   (size_t) (nstage - first_out) * L.slot,
                                                   hipMemcpyDeviceToHost, c->stream));
         }
-        HIP_OR_DIE(hipStreamSynchronize(c->stream));
-        if (op == OP_VERIFY)
-                return min_slot((const unsigned long long *) (h + L.slots_off), nslots);
-        for (i = nsrc, s = first_out; i < nptr && s >= 0; i++)
-                if (!flag[i])
-                        memcpy(dst[i - nsrc], h + L.stage_off + (size_t) s++ * L.slot, (size_t) len);
-        return ~0ull;
+        GPU_TRY(r, hipStreamSynchronize(c->stream));
+        if (op == OP_VERIFY) {
+                r.first_bad = min_slot((const unsigned long long *) (h + L.slots_off), nslots);
+        } else {
+                for (i = nsrc, s = first_out; i < nptr && s >= 0; i++)
+                        if (!flag[i])
+                                memcpy(dst[i - nsrc], h + L.stage_off + (size_t) s++ * L.slot,
+                                       (size_t) len);
+        }
+        r.done = len;
+        return r;
 }
 
-/*
- * OP_ENCODE: dst[l] = XOR_j c[l][j] * src[j], nsrc = k.
- * OP_UPDATE: dst[l] ^= c[l][vec_i] * src[0], nsrc = 1.
- * OP_VERIFY: compare dst[l] with XOR_j c[l][j] * src[j]; nothing is written.
- * Returns ~0 (no mismatch / not a verify) or the first mismatch as
- * column << 8 | row.
- */
-static unsigned long long
-run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
-       unsigned char *const *src, int nsrc, unsigned char *const *dst)
+/* Column-chunked mode: whole shards when nothing is staged, else chunks of at
+ * most stage_limit() bytes over all staged shards. r.done advances past every
+ * chunk whose outputs are final. */
+static gpu_res
+gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+            unsigned char *const *src, int nsrc, unsigned char *const *dst, const int *flag,
+            int nstage)
 {
-        unsigned long long first_bad = ~0ull;
-        ctx_t *c;
-        int nptr = nsrc + rows, i, nstage = 0;
-        int dev_flag[512];
-        int *flag, nslots;
+        gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
+        int nptr = nsrc + rows, i, nslots;
         size_t chunk, slot;
         layout_t L;
         uint64_t *h_ptrs;
         long long c0;
 
-        if (len <= 0 || rows <= 0 || k < 0)
-                return first_bad;
-        if (op == OP_UPDATE && (vec_i < 0 || vec_i >= k)) {
-                /* Out-of-range vec_i is undefined in the reference (it reads past
-                 * gftbls); here it must not become an out-of-bounds GPU access. */
-                fprintf(stderr, "isal_hip: ec update with vec_i=%d outside [0,%d): ignored\n",
-                        vec_i, k);
-                return first_bad;
-        }
-        flag = nptr <= 512 ? dev_flag : (int *) malloc(sizeof(int) * (size_t) nptr);
-        if (!flag) {
-                fprintf(stderr, "isal_hip: out of host memory\n");
-                abort();
-        }
-        c = ctx_get();
-
-        for (i = 0; i < nptr; i++) {
-                const void *p = i < nsrc ? src[i] : dst[i - nsrc];
-                flag[i] = on_device(p);
-                nstage += !flag[i];
-        }
-
-        if ((size_t) len * (size_t) nptr <= ZC_BYTES ||
-            (nstage && (size_t) len * (size_t) nstage <= PACK_BYTES)) {
-                unsigned long long r =
-                        run_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage,
-                                  (size_t) len * (size_t) nptr <= ZC_BYTES);
-                if (flag != dev_flag)
-                        free(flag);
-                return r;
-        }
-
-        /* Column chunk: whole shard when nothing is staged. */
         if (nstage) {
                 size_t per = stage_limit() / (size_t) nstage;
                 per &= ~(size_t) 4095;
@@ -409,14 +505,14 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                         per = 4096;
                 chunk = (size_t) len < per ? (size_t) len : per;
                 slot = (chunk + 255) & ~(size_t) 255; /* keep every slot 256-B aligned */
-                ensure_stage(c, slot * (size_t) nstage);
+                GPU_TRY(r, ensure_stage(c, slot * (size_t) nstage));
         } else {
                 chunk = (size_t) len;
                 slot = 0;
         }
 
         L = call_layout(op, len, k, rows, nptr, 0);
-        ensure_args(c, L.stage_off);
+        GPU_TRY(r, ensure_args(c, L.stage_off));
         h_ptrs = (uint64_t *) c->h_args;
         isal_hip_build_tables(k, rows, gftbls, (uint32_t *) ((char *) c->h_args + L.ptr_bytes));
 
@@ -434,46 +530,159 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                                 /* sources, and outputs of a read-modify-write update or
                                  * of a verify, go in */
                                 if (i < nsrc || op != OP_ENCODE)
-                                        HIP_OR_DIE(hipMemcpyAsync(st, host + c0, (size_t) clen,
+                                        GPU_TRY(r, hipMemcpyAsync(st, host + c0, (size_t) clen,
                                                                   hipMemcpyHostToDevice, c->stream));
                         }
                         h_ptrs[i] = d;
                         if (d & 15)
                                 vec16 = 0;
                 }
-                HIP_OR_DIE(hipMemcpyAsync(c->d_args, c->h_args, L.args_bytes,
+                GPU_TRY(r, hipMemcpyAsync(c->d_args, c->h_args, L.args_bytes,
                                           hipMemcpyHostToDevice, c->stream));
-                nslots = launch_op(c, op, (char *) c->d_args, &L, nptr, nsrc, clen, c0, k, rows,
-                                   vec_i, vec16);
+                GPU_TRY(r, launch_op(c, op, (char *) c->d_args, &L, nptr, nsrc, clen, c0, k, rows,
+                                     vec_i, vec16, &nslots));
                 if (op == OP_VERIFY) {
-                        HIP_OR_DIE(hipMemcpyAsync((char *) c->h_args + L.slots_off,
+                        GPU_TRY(r, hipMemcpyAsync((char *) c->h_args + L.slots_off,
                                                   (char *) c->d_args + L.slots_off,
                                                   (size_t) nslots * 8, hipMemcpyDeviceToHost,
                                                   c->stream));
-                        HIP_OR_DIE(hipStreamSynchronize(c->stream));
-                        first_bad = min_slot(
+                        GPU_TRY(r, hipStreamSynchronize(c->stream));
+                        r.first_bad = min_slot(
                                 (const unsigned long long *) ((char *) c->h_args + L.slots_off),
                                 nslots);
-                        if (first_bad != ~0ull)
+                        r.done = c0 + clen;
+                        if (r.first_bad != ~0ull)
                                 break;
                         continue;
                 }
                 s = 0; /* staged slots are in pointer order: outputs follow sources */
+                r.chunk_end = c0 + clen;
+                r.rows_out = 0;
                 for (i = 0; i < nptr; i++) {
                         if (flag[i])
                                 continue;
-                        if (i >= nsrc)
-                                HIP_OR_DIE(hipMemcpyAsync(dst[i - nsrc] + c0,
+                        if (i >= nsrc) {
+                                GPU_TRY(r, hipMemcpyAsync(dst[i - nsrc] + c0,
                                                           c->d_stage + (size_t) s * slot,
                                                           (size_t) clen, hipMemcpyDeviceToHost,
                                                           c->stream));
+                                r.rows_out = i - nsrc + 1;
+                        }
                         s++;
                 }
-                HIP_OR_DIE(hipStreamSynchronize(c->stream));
+                GPU_TRY(r, hipStreamSynchronize(c->stream));
+                r.done = c0 + clen;
+                r.rows_out = 0;
+        }
+        r.done = len;
+        return r;
+}
+
+static unsigned long long
+cpu_route(int op, long long c0, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+          unsigned char *const *src, int nsrc, unsigned char *const *dst)
+{
+        __atomic_add_fetch(&g_cpu_calls, 1ull, __ATOMIC_RELAXED);
+        return isal_cpu_run(op, c0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
+}
+
+/*
+ * OP_ENCODE: dst[l] = XOR_j c[l][j] * src[j], nsrc = k.
+ * OP_UPDATE: dst[l] ^= c[l][vec_i] * src[0], nsrc = 1.
+ * OP_VERIFY: compare dst[l] with XOR_j c[l][j] * src[j]; nothing is written.
+ * Returns ~0 (no mismatch / not a verify) or the first mismatch as
+ * column << 8 | row.
+ */
+static unsigned long long
+run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+       unsigned char *const *src, int nsrc, unsigned char *const *dst)
+{
+        const int be = backend();
+        const int nptr = nsrc + rows;
+        int dev_flag[512], *flag, i, nstage = 0, all_host;
+        size_t bytes;
+        gpu_res r;
+        ctx_t *c;
+
+        if (len <= 0 || rows <= 0 || k < 0)
+                return ~0ull;
+        if (op == OP_UPDATE && (vec_i < 0 || vec_i >= k)) {
+                /* Out-of-range vec_i is undefined in the reference (it reads past
+                 * gftbls); here it must not become an out-of-bounds GPU access. */
+                fprintf(stderr, "isal_hip: ec update with vec_i=%d outside [0,%d): ignored\n",
+                        vec_i, k);
+                return ~0ull;
+        }
+        bytes = (size_t) len * (size_t) nptr;
+        if (!gpu_present()) {
+                if (be == BACKEND_GPU) {
+                        fprintf(stderr, "isal_hip: ISAL_HIP_BACKEND=gpu but no GPU is usable\n");
+                        abort();
+                }
+                /* no HIP runtime to ask: every pointer is a host pointer */
+                route_log(op, len, k, rows, "cpu", "no GPU");
+                return cpu_route(op, 0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
+        }
+
+        flag = nptr <= 512 ? dev_flag : (int *) malloc(sizeof(int) * (size_t) nptr);
+        if (!flag) {
+                fprintf(stderr, "isal_hip: out of host memory\n");
+                abort();
+        }
+        for (i = 0; i < nptr; i++) {
+                const void *p = i < nsrc ? src[i] : dst[i - nsrc];
+                flag[i] = on_device(p);
+                nstage += !flag[i];
+        }
+        all_host = nstage == nptr;
+
+        if (all_host && (be == BACKEND_CPU || (be == BACKEND_AUTO && bytes <= cpu_max_bytes()))) {
+                if (flag != dev_flag)
+                        free(flag);
+                route_log(op, len, k, rows, "cpu", be == BACKEND_CPU ? "ISAL_HIP_BACKEND=cpu" : "small host call");
+                return cpu_route(op, 0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
+        }
+
+        c = ctx_get(&r.err, &r.what);
+        if (!c) {
+                r.done = 0;
+                r.first_bad = ~0ull;
+        } else if (bytes <= ZC_BYTES || (nstage && (size_t) len * (size_t) nstage <= PACK_BYTES)) {
+                const int zc = bytes <= ZC_BYTES;
+                route_log(op, len, k, rows, zc ? "gpu zero-copy" : "gpu packed",
+                          all_host ? "host shards" : "device shards");
+                r = gpu_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage, zc);
+        } else {
+                route_log(op, len, k, rows, nstage ? "gpu chunked" : "gpu device-resident",
+                          all_host ? "host shards" : "device shards");
+                r = gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage);
         }
         if (flag != dev_flag)
                 free(flag);
-        return first_bad;
+        if (r.err == hipSuccess)
+                return r.first_bad;
+        if (!all_host || be == BACKEND_GPU)
+                die(r.what, r.err);
+        (void) hipGetLastError();
+        report_fallback(r.what, r.err);
+        /* nothing queued may still write our outputs */
+        if (c && hipStreamSynchronize(c->stream) != hipSuccess && op == OP_UPDATE && r.rows_out)
+                die("hipStreamSynchronize after a failed update (parity state unknown)", r.err);
+        if (op == OP_UPDATE && r.rows_out) {
+                /* rows [0, rows_out) of [done, chunk_end) are already updated */
+                unsigned char *s1 = src[0] + r.done, **d1;
+                const int nr = rows - r.rows_out;
+                d1 = (unsigned char **) malloc(sizeof(*d1) * (size_t) (nr > 0 ? nr : 1));
+                if (!d1)
+                        abort();
+                for (i = 0; i < nr; i++)
+                        d1[i] = dst[r.rows_out + i] + r.done;
+                (void) cpu_route(op, 0, (int) (r.chunk_end - r.done), k, nr, vec_i,
+                                 gftbls + (size_t) r.rows_out * k * 32, &s1, 1, d1);
+                free(d1);
+                r.done = r.chunk_end;
+        }
+        return cpu_route(op, r.done, len, k, rows, vec_i, gftbls, src, nsrc, dst);
 }
 
 unsigned long long
@@ -569,10 +778,11 @@ struct isal_hip_batch {
          * and the per-lane partials (crc_kernels.hip) */
         isal_hip_crc_geom crc;
         uint32_t *d_crc, *d_part, *d_tail;
-        /* CRC64 state, allocated on first use: the table set of the last
-         * variant used (c64_variant) and the per-lane chains */
-        int c64_variant, c64_tt;
-        uint64_t *d_c64tab, *d_c64part;
+        /* CRC64 state, allocated on first use: one table set per variant
+         * used (never overwritten, so switching variants needs no device
+         * synchronisation) and the per-lane chains */
+        int c64_tt;
+        uint64_t *d_c64tab[ISAL_HIP_CRC64_NVARIANTS], *d_c64part;
 };
 
 int
@@ -639,11 +849,19 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         if (!h)
                 return ISAL_HIP_ENOMEM;
         isal_hip_build_tables(b->k, b->rows, gftbls, h);
-        if (!b->d_tbl && hipMalloc((void **) &b->d_tbl, n * 4 + 4) != hipSuccess) {
-                free(h);
-                return ISAL_HIP_EHIP;
+        if (!b->d_tbl) {
+                if (hipMalloc((void **) &b->d_tbl, n * 4 + 4) != hipSuccess) {
+                        free(h);
+                        return ISAL_HIP_EHIP;
+                }
+                e = hipSuccess;
+        } else {
+                /* launches already queued on any (possibly non-blocking) stream may
+                 * still read the old coefficients: let them finish first */
+                e = hipDeviceSynchronize();
         }
-        e = hipMemcpy(b->d_tbl, h, n * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+                e = hipMemcpy(b->d_tbl, h, n * 4, hipMemcpyHostToDevice);
         free(h);
         return e == hipSuccess ? ISAL_HIP_OK : ISAL_HIP_EHIP;
 }
@@ -683,8 +901,9 @@ isal_hip_batch_destroy(isal_hip_batch *b)
                 (void) hipFree(b->d_crc);
         if (b->d_part)
                 (void) hipFree(b->d_part);
-        if (b->d_c64tab)
-                (void) hipFree(b->d_c64tab);
+        for (int v = 0; v < ISAL_HIP_CRC64_NVARIANTS; v++)
+                if (b->d_c64tab[v])
+                        (void) hipFree(b->d_c64tab[v]);
         if (b->d_c64part)
                 (void) hipFree(b->d_c64part);
         free(b);
@@ -698,12 +917,12 @@ isal_hip_batch_destroy(isal_hip_batch *b)
 static int
 crc_tiles(int len, int nstripes)
 {
-        const char *e = getenv("ISAL_HIP_CRC_TILES");
+        const long long knob = isal_hip_knob(ISAL_HIP_KNOB_CRC_TILES);
         long long ntiles = ((long long) len + ISAL_HIP_CRC_TILE - 1) / ISAL_HIP_CRC_TILE;
-        int tt = e ? atoi(e) : 16;
+        int tt = knob >= 0 ? (int) knob : 16;
         if (tt < 1)
                 tt = 1;
-        if (e)
+        if (knob >= 0)
                 return tt;
         while (tt > 1 && (long long) nstripes * ((ntiles + tt - 1) / tt) < 2048)
                 tt /= 2;
@@ -790,38 +1009,41 @@ static int
 batch_crc64_setup(isal_hip_batch *b, int variant)
 {
         isal_hip_crc64_geom g;
-        uint64_t *h;
+        uint64_t *h, *d = NULL;
         hipError_t e;
         const size_t tab = ISAL_HIP_CRC64_TAB_ENTRIES;
-        if (b->d_c64tab && b->c64_variant == variant)
+        if (b->d_c64tab[variant])
                 return ISAL_HIP_OK;
-        if (!b->d_c64tab) {
+        if (!b->d_c64part && !b->c64_tt) {
                 b->c64_tt = crc_tiles(b->len, b->nstripes);
                 isal_hip_crc64_geometry(b->len, b->c64_tt, &g);
-                e = hipMalloc((void **) &b->d_c64tab, tab * 8);
-                if (e == hipSuccess && g.nblk)
+                if (g.nblk) {
                         e = hipMalloc((void **) &b->d_c64part, (size_t) b->nstripes *
                                                                        (size_t) (b->k + b->rows) *
                                                                        (size_t) g.nblk * 256 * 8);
-                if (e != hipSuccess) {
-                        if (b->d_c64tab)
-                                (void) hipFree(b->d_c64tab);
-                        b->d_c64tab = b->d_c64part = NULL;
-                        return e == hipErrorOutOfMemory ? ISAL_HIP_ENOMEM : ISAL_HIP_EHIP;
+                        if (e != hipSuccess) {
+                                b->d_c64part = NULL;
+                                b->c64_tt = 0; /* retry the whole setup next time */
+                                return e == hipErrorOutOfMemory ? ISAL_HIP_ENOMEM : ISAL_HIP_EHIP;
+                        }
                 }
         }
         h = (uint64_t *) malloc(tab * 8);
         if (!h)
                 return ISAL_HIP_ENOMEM;
         isal_hip_crc64_tables(variant, b->len, b->c64_tt, h);
-        /* the previous variant's launches may still read the old tables */
-        e = hipDeviceSynchronize();
+        /* a fresh buffer per variant: launches of other variants queued on any
+         * stream keep reading their own tables */
+        e = hipMalloc((void **) &d, tab * 8);
         if (e == hipSuccess)
-                e = hipMemcpy(b->d_c64tab, h, tab * 8, hipMemcpyHostToDevice);
+                e = hipMemcpy(d, h, tab * 8, hipMemcpyHostToDevice);
         free(h);
-        if (e != hipSuccess)
-                return ISAL_HIP_EHIP;
-        b->c64_variant = variant;
+        if (e != hipSuccess) {
+                if (d)
+                        (void) hipFree(d);
+                return e == hipErrorOutOfMemory ? ISAL_HIP_ENOMEM : ISAL_HIP_EHIP;
+        }
+        b->d_c64tab[variant] = d; /* published only once filled */
         return ISAL_HIP_OK;
 }
 
@@ -836,7 +1058,7 @@ isal_hip_batch_crc64(isal_hip_batch *b, int variant, unsigned long long init,
                 return r;
         return isal_hip_launch_crc64(b->d_ptrs, b->k + b->rows, b->k + b->rows, b->nstripes,
                                      b->len, b->vec16, isal_hip_crc64_is_refl(variant), b->c64_tt,
-                                     b->d_c64tab, b->d_c64part,
+                                     b->d_c64tab[variant], b->d_c64part,
                                      isal_hip_crc64_init_term(variant, b->len, init),
                                      (uint64_t *) crc, stream)
                        ? ISAL_HIP_EHIP
@@ -855,11 +1077,11 @@ isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long i
                 return r;
         isal_hip_crc64_geometry(b->len, b->c64_tt, &g);
         if (b->vec16 && b->len % 16 == 0 && g.nblk > 0 && b->rows <= EC_MAX_ROWS_PER_PASS &&
-            b->k <= ISAL_HIP_CRC64_MAX_FUSED_K)
+            b->k >= 1 && b->k <= ISAL_HIP_CRC64_MAX_FUSED_K)
                 /* one pass over the stripe: encode + CRC64 of all k + rows shards */
                 return isal_hip_launch_encode_crc64(
                                b->d_ptrs, b->k, b->rows, b->nstripes, b->len, b->d_tbl,
-                               isal_hip_crc64_is_refl(variant), b->c64_tt, b->d_c64tab,
+                               isal_hip_crc64_is_refl(variant), b->c64_tt, b->d_c64tab[variant],
                                b->d_c64part, isal_hip_crc64_init_term(variant, b->len, init),
                                (uint64_t *) crc, stream)
                        ? ISAL_HIP_EHIP
@@ -880,7 +1102,7 @@ isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *cr
                 return batch_crc_empty(b, init, crc, stream);
         if ((r = batch_crc_setup(b)) != ISAL_HIP_OK)
                 return r;
-        if (b->vec16 && b->len % 16 == 0 && b->k <= ISAL_HIP_CRC_MAX_FUSED_K) {
+        if (b->vec16 && b->len % 16 == 0 && b->k >= 1 && b->k <= ISAL_HIP_CRC_MAX_FUSED_K) {
                 /* one pass over the stripe: encode + CRC of all k + rows shards */
                 if (isal_hip_launch_encode_crc(b->d_ptrs, b->k + b->rows, 0, b->k, b->d_tbl, b->len,
                                                b->k, b->rows, b->nstripes, b->crc.tt, b->d_crc,

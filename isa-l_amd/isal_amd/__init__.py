@@ -7,9 +7,11 @@ include/gf_vect_mul.h), so tests and the benchmark read like the reference's
 own C tests. Buffers may be numpy uint8 arrays (host memory), torch tensors
 (host or device; their storage address is passed), or raw integer addresses.
 
-There is no fallback: importing works without a GPU (host-side functions such
-as gf_mul or ec_init_tables need none), but every data-path call goes to the
-GPU through the library, and a missing library raises immediately.
+There is no Python fallback: every data-path call goes through the library
+(a missing library raises immediately). The library itself routes each
+drop-in call (include/isal_hip.h "routing"): device-resident shards and large
+host calls to the GPU kernels, small host calls to its CPU route;
+ISAL_HIP_BACKEND=gpu forces the kernels.
 """
 from __future__ import annotations
 
@@ -25,7 +27,7 @@ __all__ = [
     "ec_encode_data_base", "ec_encode_data_update", "ec_encode_data_update_base",
     "gf_vect_dot_prod", "gf_vect_dot_prod_base", "gf_vect_mad", "gf_vect_mad_base",
     "gf_vect_mul", "gf_vect_mul_base", "Batch", "Pipe", "kernel_launches", "max_rows_per_pass",
-    "version", "addr",
+    "version", "addr", "cpu_calls", "fallbacks", "reload_config",
 ]
 
 LIB_PATH = os.environ.get(
@@ -107,6 +109,9 @@ def lib() -> ctypes.CDLL:
             "isal_hip_pipe_flush": (i, [ctypes.c_void_p]),
             "isal_hip_pipe_destroy": (i, [ctypes.c_void_p]),
             "isal_hip_kernel_launches": (ctypes.c_ulonglong, []),
+            "isal_hip_cpu_calls": (ctypes.c_ulonglong, []),
+            "isal_hip_fallbacks": (ctypes.c_ulonglong, []),
+            "isal_hip_config_reload": (None, []),
             "isal_hip_max_rows_per_pass": (i, []),
             "isal_hip_target": (ctypes.c_char_p, []),
         }
@@ -360,14 +365,6 @@ class Pipe:
         if rc != 0:
             raise RuntimeError(f"isal_hip_pipe_flush failed ({rc})")
 
-    def encode_crc64(self, variant: int, init: int, crc, stream: int = 0) -> None:
-        """encode() plus crc64_<variant>(init, shard, len) of every source and
-        parity shard, layout as crc64(); one pass over HBM where the shape allows."""
-        rc = lib().isal_hip_batch_encode_crc64(self._h, variant, init & 0xFFFFFFFFFFFFFFFF,
-                                               ctypes.c_void_p(addr(crc)), ctypes.c_void_p(stream))
-        if rc != 0:
-            raise RuntimeError(f"isal_hip_batch_encode_crc64 failed ({rc})")
-
     def close(self) -> None:
         if getattr(self, "_h", None):
             lib().isal_hip_pipe_destroy(self._h)
@@ -382,6 +379,22 @@ class Pipe:
 
 def kernel_launches() -> int:
     return int(lib().isal_hip_kernel_launches())
+
+
+def cpu_calls() -> int:
+    """Drop-in calls the library served on its CPU route (small host calls,
+    ISAL_HIP_BACKEND=cpu, no GPU, HIP-failure fallbacks)."""
+    return int(lib().isal_hip_cpu_calls())
+
+
+def fallbacks() -> int:
+    """Drop-in calls that hit a HIP failure and finished on the CPU route."""
+    return int(lib().isal_hip_fallbacks())
+
+
+def reload_config() -> None:
+    """Re-read the ISAL_HIP_* environment knobs (read once otherwise)."""
+    lib().isal_hip_config_reload()
 
 
 def max_rows_per_pass() -> int:

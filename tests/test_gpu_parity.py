@@ -19,6 +19,32 @@ from ecutil import coeffs, fill_bytes, golden
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _force_gpu_route(engine):
+    """Every drop-in call in this module runs the GPU kernels, whatever its size
+    (the library's default would send small host calls to its CPU route)."""
+    with pytest.MonkeyPatch.context() as mp:
+        mp.setenv("ISAL_HIP_BACKEND", "gpu")
+        engine.reload_config()
+        yield
+    engine.reload_config()
+
+
+@pytest.fixture(autouse=True)
+def _reload_knobs_after(engine):
+    """Knobs are read once by the library: tests that change one re-read them
+    (_setenv), and every test leaves the library re-synced with os.environ."""
+    yield
+    engine.reload_config()
+
+
+def _setenv(monkeypatch, name, value):
+    import isal_amd
+
+    monkeypatch.setenv(name, value)
+    isal_amd.reload_config()
+
+
 def _h(s):
     return np.frombuffer(bytes.fromhex(s), dtype=np.uint8)
 
@@ -270,11 +296,29 @@ def test_config_c1_cauchy_k4_p2_64k(engine, gpu):
     assert [ecutil.oracle().fnv(d) for d in dst] == case["fnv"]
 
 
+def _oracle_encode_all(oracle, coef, k, rows, srcs, threads=16):
+    """Oracle parity of many stripes at once: srcs[s] = list of k host arrays.
+    ctypes releases the GIL inside the oracle, so the stripes run in parallel
+    on the host cores (the oracle is the checker, never the code under test)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    tbls = oracle.ec_init_tables(k, rows, coef)
+    n = len(srcs[0][0])
+
+    def one(src):
+        dst = [np.zeros(n, np.uint8) for _ in range(rows)]
+        oracle.ec_encode_data(n, k, rows, tbls, src, dst)
+        return dst
+
+    with ThreadPoolExecutor(max_workers=min(threads, os.cpu_count() or 1)) as ex:
+        return list(ex.map(one, srcs))
+
+
 def test_config_c2_c3_full_size(engine, oracle, gpu):
     """C2: k=10 p=4, 1 MiB shards x 1024 stripes in one launch; C3: recover 3
-    erased data shards {4,6,7} of every stripe. Full size, checked by properties:
-    decode(encode(x)) == x for every stripe, parity row 0 == XOR of the sources
-    (all-ones Vandermonde row), and oracle byte-for-byte on sampled stripes."""
+    erased data shards {4,6,7} of every stripe. Full size and byte for byte:
+    all 1024 x 4 parity shards == the oracle, all 1024 x 3 recovered shards ==
+    the oracle's decode of the same survivors, and == the erased data."""
     import torch
 
     k, p, n, ns = 10, 4, 1 << 20, 1024
@@ -283,15 +327,12 @@ def test_config_c2_c3_full_size(engine, oracle, gpu):
     enc = engine.Batch(n, k, p, engine.ec_init_tables(k, p, a[k * k:]), ns, dptr, cptr)
     enc.encode(0)
     torch.cuda.synchronize()
-    x = data[:, 0].clone()
-    for j in range(1, k):
-        x ^= data[:, j]
-    assert torch.equal(x, coding[:, 0])
-    del x
-    for s in (0, 511, 1023):
-        want = oracle.encode(a[k * k:], k, p, [_host(data[s, j]) for j in range(k)])
+    h_data, h_cod = _host(data), _host(coding)
+    want = _oracle_encode_all(oracle, a[k * k:], k, p, [[h_data[s, j] for j in range(k)] for s in range(ns)])
+    for s in range(ns):
         for l in range(p):
-            assert np.array_equal(_host(coding[s, l]), want[l]), (s, l)
+            assert np.array_equal(h_cod[s, l], want[s][l]), (s, l)
+    del want
     errs = [4, 6, 7]
     ret, c, surv = ecutil.decode_matrix(a, k, errs)
     assert ret == 0
@@ -302,10 +343,40 @@ def test_config_c2_c3_full_size(engine, oracle, gpu):
     dec = engine.Batch(n, k, len(errs), engine.ec_init_tables(k, len(errs), c), ns, sptr, rptr)
     dec.encode(0)
     torch.cuda.synchronize()
-    for i, e in enumerate(errs):
-        assert torch.equal(rec[:, i], data[:, e]), e
+    h_rec = _host(rec)
+    hfrag = lambda s, i: h_data[s, i] if i < k else h_cod[s, i - k]  # noqa: E731
+    want = _oracle_encode_all(oracle, c, k, len(errs), [[hfrag(s, i) for i in surv] for s in range(ns)])
+    for s in range(ns):
+        for i, e in enumerate(errs):
+            assert np.array_equal(h_rec[s, i], want[s][i]), (s, e)
+            assert np.array_equal(h_rec[s, i], h_data[s, e]), (s, e)
     enc.close()
     dec.close()
+
+
+def test_dropin_call_ordered_after_default_stream_work(engine, oracle, gpu):
+    """A synchronous drop-in call on device shards sees work the caller queued
+    on the legacy default stream just before it (torch writes the sources and
+    clears the outputs, asynchronously) — the engine's stream is blocking."""
+    import torch
+
+    k, rows, n = 10, 4, 8 << 20
+    coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+    tbls = engine.ec_init_tables(k, rows, coef)
+    src = torch.zeros((k, n), dtype=torch.uint8, device=gpu)
+    out = torch.full((rows, n), 0x77, dtype=torch.uint8, device=gpu)
+    for it in range(3):
+        # long default-stream kernels right before the call
+        src.random_(generator=torch.Generator(device=gpu).manual_seed(it))
+        src.bitwise_xor_(torch.full_like(src, 0x5A))
+        out.fill_(0x33)
+        engine.ec_encode_data(n, k, rows, tbls, [src[j] for j in range(k)], [out[l] for l in range(rows)])
+        h = _host(src)
+        win = slice(n - 65536, n)  # the last columns: written last by torch
+        want = oracle.encode(coef, k, rows, [h[j, win] for j in range(k)])
+        got = _host(out[:, win])
+        for l in range(rows):
+            assert np.array_equal(got[l], want[l]), (it, l)
 
 
 # --------------------------------------------------------------------------
@@ -384,7 +455,7 @@ def test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, k, rows, n, 
     import torch
 
     if tt:
-        monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+        _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
     a = oracle.gf_gen_rs_matrix(k + rows, k)
     tbls = engine.ec_init_tables(k, rows, a[k * k:].copy())
     bufs = [fill_bytes(n, 7919 * s + j + variant) for s in range(ns) for j in range(k + rows)]
@@ -431,9 +502,9 @@ def test_crc_chain_step(engine, oracle, gpu, monkeypatch, step, k, rows, n, ns, 
     count is not a multiple of the load batch."""
     import torch
 
-    monkeypatch.setenv("ISAL_HIP_CRC_STEP", str(step))
+    _setenv(monkeypatch, "ISAL_HIP_CRC_STEP", str(step))
     if tt:
-        monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+        _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
     a = oracle.gf_gen_rs_matrix(k + rows, k)
     tbls = engine.ec_init_tables(k, rows, a[k * k:].copy())
     bufs = [fill_bytes(n, 17 * s + j + step) for s in range(ns) for j in range(k + rows)]
@@ -501,7 +572,7 @@ def test_encode_crc_tiles_per_workgroup(engine, oracle, gpu, monkeypatch, k, row
     partial last blocks (23 full tiles % tt) and the ragged tile."""
     import torch
 
-    monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+    _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
     n, ns = 4096 * 23 + 2048, 3
     a = oracle.gf_gen_rs_matrix(k + rows, k)
     coef = a[k * k:].copy()
@@ -602,10 +673,10 @@ def test_crc64_chain_step(engine, oracle, gpu, monkeypatch, step, batch, k, rows
     a multiple of the step."""
     import torch
 
-    monkeypatch.setenv("ISAL_HIP_CRC64_STEP", str(step))
-    monkeypatch.setenv("ISAL_HIP_CRC64_BATCH", str(batch))
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_STEP", str(step))
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_BATCH", str(batch))
     if tt:
-        monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+        _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
     a = oracle.gf_gen_rs_matrix(k + rows, k)
     tbls = engine.ec_init_tables(k, rows, a[k * k:].copy())
     bufs = [fill_bytes(n, 31 * s + j + step) for s in range(ns) for j in range(k + rows)]
@@ -644,7 +715,7 @@ def test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns
     import torch
 
     if tt:
-        monkeypatch.setenv("ISAL_HIP_CRC_TILES", str(tt))
+        _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
     a = oracle.gf_gen_rs_matrix(k + rows, k)
     coef = a[k * k:].copy()
     tbls = engine.ec_init_tables(k, rows, coef)
@@ -683,8 +754,8 @@ def test_encode_crc64_knobs(engine, oracle, gpu, monkeypatch, pair, chain, k, ro
     """The fused encode + CRC64 kernel with unpaired chain steps
     (ISAL_HIP_CRC64_FUSED_PAIR=0) and with register source chains
     (ISAL_HIP_CRC64_SRC_CHAIN=reg) == oracle as the defaults are."""
-    monkeypatch.setenv("ISAL_HIP_CRC64_FUSED_PAIR", str(pair))
-    monkeypatch.setenv("ISAL_HIP_CRC64_SRC_CHAIN", chain)
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_PAIR", str(pair))
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_SRC_CHAIN", chain)
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant)
 
 
@@ -740,6 +811,31 @@ def test_config_c4_streaming_update_k20_p6(engine, oracle, gpu):
         assert np.array_equal(_host(coding[0, l, lo:hi]), want[l])
 
 
+def test_config_c4_pipeline_full_shape_vs_oracle(engine, oracle, gpu):
+    """C4 through the host-memory pipeline at its real shape: k=20 p=6, 4 MiB
+    pinned host shards, 4 stripes, update mode (each source folded as it lands)
+    with H2D / compute / D2H overlapped — every parity byte == the oracle
+    (erasure_code_update_test.c:320-333: update must equal ec_encode_data)."""
+    import torch
+
+    k, p, n, ns = 20, 6, 4 << 20, 4
+    a = engine.gf_gen_rs_matrix(k + p, k)
+    tbls = engine.ec_init_tables(k, p, a[k * k:])
+    src = torch.empty((ns, k, n), dtype=torch.uint8).pin_memory()
+    src.random_(generator=torch.Generator().manual_seed(404))
+    par = torch.full((ns, p, n), 0xEE, dtype=torch.uint8).pin_memory()
+    pipe = engine.Pipe(n, k, p, tbls, depth=3, mode="update")
+    for s in range(ns):
+        pipe.submit([src[s, j] for j in range(k)], [par[s, l] for l in range(p)])
+    pipe.flush()
+    pipe.close()
+    h = src.numpy()
+    want = _oracle_encode_all(oracle, a[k * k:], k, p, [[h[s, j] for j in range(k)] for s in range(ns)])
+    for s in range(ns):
+        for l in range(p):
+            assert np.array_equal(par[s, l].numpy(), want[s][l]), (s, l)
+
+
 # --------------------------------------------------------------------------
 # the reference's own test programs, linked against libisal_hip.so
 # --------------------------------------------------------------------------
@@ -751,17 +847,19 @@ CONFORMANCE = ["gf_inverse_test", "gf_vect_mul_test", "gf_vect_mul_base_test",
 
 
 # xor_check_test / pq_check_test sweep every (length, error position, vector)
-# with ~1.6e7 synchronous calls each; at a ~25-30 us GPU round trip per call
-# that is ~8-10 minutes apiece, so they run only with ISAL_SLOW_CONFORMANCE=1
-# (their logs: profiles/r01_slow_conformance.log).
+# with ~1.6e7 small synchronous calls each: at a ~30 us GPU round trip per call
+# that is ~10 minutes apiece, so under ISAL_HIP_BACKEND=gpu they run only with
+# ISAL_SLOW_CONFORMANCE=1 (logs: profiles/r01_slow_conformance_*.log). Under
+# the library's default routing (auto: small host calls on the CPU route, the
+# rest on the GPU) all thirteen run.
 SLOW_CONFORMANCE = {"xor_check_test", "pq_check_test"}
 
 
-def _run_streaming(exe, timeout):
+def _run_streaming(exe, timeout, env=None):
     """Run a test program, echoing a heartbeat so long runs visibly progress."""
     import time
 
-    p = subprocess.Popen([exe], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    p = subprocess.Popen([exe], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
     t0 = time.time()
     out = []
     while True:
@@ -779,14 +877,15 @@ def _run_streaming(exe, timeout):
     return p.returncode, "".join(out)
 
 
+@pytest.mark.parametrize("backend", ["gpu", "auto"])
 @pytest.mark.parametrize("name", CONFORMANCE)
-def test_reference_test_programs(name, gpu):
-    if name in SLOW_CONFORMANCE and not os.environ.get("ISAL_SLOW_CONFORMANCE"):
-        pytest.skip("~1.6e7 synchronous calls; set ISAL_SLOW_CONFORMANCE=1")
+def test_reference_test_programs(name, backend, gpu):
+    if backend == "gpu" and name in SLOW_CONFORMANCE and not os.environ.get("ISAL_SLOW_CONFORMANCE"):
+        pytest.skip("~1.6e7 synchronous GPU round trips; set ISAL_SLOW_CONFORMANCE=1 (auto runs it)")
     exe = os.path.join(ecutil.REF_DIR, "conformance", name)
     if not os.path.exists(exe):
         pytest.skip(f"{name} not built (make -C oracle conformance needs /root/reference)")
-    rc, out = _run_streaming(exe, timeout=1500)
+    rc, out = _run_streaming(exe, timeout=1500, env=dict(os.environ, ISAL_HIP_BACKEND=backend))
     assert rc == 0, out[-3000:]
     assert "Pass" in out or "pass" in out.lower()
 

@@ -119,6 +119,31 @@ for s in $STEPS; do
         probe)
                 run probe 300 isa-l_amd/build/ec_probe
                 ;;
+        refcpu)
+                # the reference's own perf harnesses on the host cores (no GPU)
+                run refcpu_encode 200 python3 tools/cpu_ref_baseline.py --which encode
+                cp "$OUT/refcpu_encode.log" "$OUT/refcpu_encode.json"
+                run refcpu_update 300 python3 tools/cpu_ref_baseline.py --which update
+                cp "$OUT/refcpu_update.log" "$OUT/refcpu_update.json"
+                ;;
+        decodeprof|updateprof)
+                if [ $s = decodeprof ]; then
+                        wl=decode; args="--workload decode"; kern=ec_encode_v16; cfg="workload=decode k=10 p=4 len=1048576 stripes=1024"
+                else
+                        wl=update; args="--workload update --k 20 --p 6 --len 4194304 --stripes 64"; kern=ec_update_v16; cfg="workload=update k=20 p=6 len=4194304 stripes=64"
+                fi
+                run bench_$wl 300 python bench.py $args --cpu-seconds 5
+                cp "$OUT/bench_$wl.log" "$OUT/bench_$wl.json"
+                run rocprof_$wl 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$wl" -o $wl -- python3 bench.py $args --no-cpu-baseline
+                run pmc_fetch_$wl 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$wl" -o f -- python3 bench.py $args --no-cpu-baseline --steps 3 --warmup 1
+                run pmc_write_$wl 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$wl" -o w -- python3 bench.py $args --no-cpu-baseline --steps 3 --warmup 1
+                python3 tools/pmc_csv.py "$OUT/pmc_$wl.csv" "$cfg" "python bench.py $args --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_$wl" "$OUT/pmc_write_$wl" $kern
+                ;;
+        e2esweep)
+                for dp in ${E2E_DEPTHS:-2 3 4 6}; do
+                        run bench_e2e_encode_d$dp 300 python bench.py --workload e2e-encode --steps 200 --warmup 10 --depth $dp
+                done
+                ;;
         *)
                 echo "unknown step $s"
                 exit 2
