@@ -55,8 +55,18 @@ def parse_args(argv=None):
                     default="encode",
                     help="e2e-*: host-resident (pinned) stripes streamed through the pipeline")
     ap.add_argument("--depth", type=int, default=3, help="e2e pipeline depth (stripes in flight)")
+    ap.add_argument("--ring", type=int, default=0,
+                    help="e2e: distinct pinned host stripes cycled through (0 = max(2*depth, 4))")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all cores of this rank (<=16)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads / pinned processes for the CPU baselines; 0 = min(16, this "
+                         "process's CPUs) — 16 is the GPU box's CPU share per GPU")
+    ap.add_argument("--cold-ring", type=int, default=8,
+                    help="distinct stripes each thread of the cold-cache SIMD-port baseline cycles over")
+    ap.add_argument("--total-stripes", type=int, default=0,
+                    help="C5 mode: this many stripes in total, split into contiguous ranges over the "
+                         "ranks (isal_hip_multi_partition); a step encodes every rank's range as a loop "
+                         "of device-resident --stripes batches (strong scaling). 0 = C2 weak scaling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N>1 control-plane backend (nccl = RCCL over xGMI; gloo lets several "
@@ -134,6 +144,16 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def sum_i64(self, xs):
+        """Element-wise SUM over ranks of a list of int64 (RCCL all-reduce)."""
+        if not self.dist:
+            return [int(x) for x in xs]
+        import torch
+
+        t = torch.tensor([int(x) for x in xs], dtype=torch.int64, device=self._dev())
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return [int(v) for v in t.cpu().tolist()]
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
@@ -209,7 +229,7 @@ def pmc_traffic(workload, k, p, n, S, kernel):
 # CPU baseline: the reference's own ec_encode_data on this host
 # ---------------------------------------------------------------------------
 
-def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=False, encode=True):
+def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=False, encode=True, ring=1):
     """Times the reference ec_encode_data (oracle/_ref/libisal_ref.so: ec_base.c +
     ec_base_aliases.c compiled from /root/reference) on `threads` host threads,
     each encoding its own k x n stripe repeatedly for ~`seconds`.
@@ -304,15 +324,19 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=Fa
 
     counts = [0] * threads
     rng = np.random.default_rng(1)
-    bufs = [([rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)],
-             [np.zeros(n, np.uint8) for _ in range(p)]) for _ in range(threads)]
+    # ring > 1: each thread cycles over `ring` distinct stripes (cold caches)
+    bufs = [[([rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)],
+              [np.zeros(n, np.uint8) for _ in range(p)]) for _ in range(ring)] for _ in range(threads)]
     deadline = time.perf_counter() + seconds
 
     def worker(i):
-        src, dst = ptrs(bufs[i][0]), ptrs(bufs[i][1])
+        srcs = [ptrs(b[0]) for b in bufs[i]]
+        dsts = [ptrs(b[1]) for b in bufs[i]]
         t = tbls.ctypes.data_as(u8p)
-        shards = [b.ctypes.data_as(u8p) for b in bufs[i][0] + bufs[i][1]]
+        shards = [b.ctypes.data_as(u8p) for b in bufs[i][0][0] + bufs[i][0][1]]
         while time.perf_counter() < deadline:
+            r = counts[i] % ring
+            src, dst = srcs[r], dsts[r]
             if encode:
                 enc(n, k, p, t, src, dst)  # ctypes drops the GIL for the call
             if crc == "crc64":
@@ -335,9 +359,205 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=Fa
         "cores": threads,
         "kind": kind,
         "sample": f"{stripes} stripes of k={k} p={p} x {n} B, {what}, "
-                  f"{threads} threads x {wall:.1f} s",
+                  f"{threads} threads x {wall:.1f} s"
+                  + (f", each thread cycling over {ring} distinct stripes (cold caches)" if ring > 1
+                     else ", each thread re-encoding one cache-warm stripe"),
         "parity_stripe_match": parity_ok,
     }
+
+
+def ref_harness_baseline(workload, k, p, n, procs):
+    """The reference's OWN perf harness on this host's cores
+    (tools/cpu_ref_baseline.py): erasure_code_perf.c (C2 encode / C3 decode,
+    -k 10 -p 4 -e 3 -s 1M) or erasure_code_update_perf.c at the C4 shape, built
+    from /root/reference by `make -C oracle ref` on its portable ec_base.c (the
+    image has no nasm for the AVX-512/GFNI kernels). Single-threaded by design,
+    so it runs once on one core and once as `procs` pinned processes at once,
+    MB/s summed. None when the shape is not one the harness takes."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import cpu_ref_baseline as crb
+
+    if workload in ("encode", "decode") and (k, p, n) == (10, 4, 1 << 20):
+        which, phase, factor = "encode", workload, 1.0
+        conv = ""
+    elif workload == "update" and (k, p, n) == (20, 6, 4 << 20):
+        # the harness counts (p+1)*len per single-source update call
+        # (erasure_code_update_perf.c:348); this bench counts the (1+2p)*len
+        # read-modify-write bytes of the same call
+        which, phase, factor = "update", "update_single_src", (1 + 2 * p) / (p + 1)
+        conv = f", converted from its (p+1)*len to this bench's (1+2p)*len bytes per call"
+    else:
+        return None
+    one, many = crb.run(which, 1), crb.run(which, procs)
+    if "error" in one or "error" in many or phase not in many or phase not in one:
+        return {"error": one.get("error") or many.get("error") or "phase missing"}
+    host = crb.host_info()
+    gib = lambda mb: round(mb * 1e6 * factor / GIB, 3)  # noqa: E731
+    per_core = one[phase]["mb_s_sum"]
+    res = {
+        "value": gib(many[phase]["mb_s_sum"]),
+        "unit": "GiB/s",
+        "cores": many["procs"],
+        "kind": "reference",
+        "sample": f"{many['command']} ({phase} phase): {many['procs']} pinned processes x ~3 s "
+                  f"(BENCHMARK_TIME), MB/s summed{conv}; reference ec_base.c path (no nasm: the "
+                  f"AVX-512/GFNI kernels cannot be assembled)",
+        "single_core_gib_s": gib(per_core),
+        "host": {a: host.get(a) for a in ("model", "sockets", "physical_cores", "cpus", "isa", "nasm")},
+    }
+    if host.get("physical_cores"):
+        # the box grants this job a 16-CPU share of the host; the whole host
+        # would give at most per-core x physical cores
+        res["all_physical_cores_est_gib_s"] = round(res["single_core_gib_s"] * host["physical_cores"], 2)
+    return res
+
+
+def ref_parity_check(k, rows, n, coef, src_host, parity_gpu):
+    """The reference's own ec_encode_data (oracle/_ref/libisal_ref.so) on one
+    stripe must give the GPU's bytes. None when the reference build is absent."""
+    import numpy as np
+
+    path = os.path.join(REPO, "oracle", "_ref", "libisal_ref.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    u8p = ctypes.POINTER(ctypes.c_ubyte)
+    tbls = np.zeros(32 * k * rows, np.uint8)
+    coef = np.ascontiguousarray(coef, dtype=np.uint8)
+    L.ec_init_tables(k, rows, coef.ctypes.data_as(u8p), tbls.ctypes.data_as(u8p))
+    out = [np.zeros(n, np.uint8) for _ in range(rows)]
+    src = [np.ascontiguousarray(s) for s in src_host]
+
+    def pp(bufs):
+        arr = (u8p * len(bufs))()
+        for i, b in enumerate(bufs):
+            arr[i] = b.ctypes.data_as(u8p)
+        return arr
+
+    L.ec_encode_data(n, k, rows, tbls.ctypes.data_as(u8p), pp(src), pp(out))
+    return all(np.array_equal(out[l], parity_gpu[l]) for l in range(rows))
+
+
+def total_stripes_run(args, d: Dist, a, k, p, n):
+    """C5 (BASELINE configs[4]): args.total_stripes stripes in all, rank r owns
+    the contiguous range isal_hip_multi_partition(T, W, r) and encodes it from
+    its own HBM as a loop of device-resident batches of args.stripes stripes
+    (the reference perf apps' re-encode-resident-buffers convention,
+    erasure_code_perf.c:126-132; every stripe-encode is counted). One step =
+    every rank encodes its whole range once. RCCL carries only the control
+    plane: matrix broadcast, barrier, max of the timings, sums of the stripe
+    counts and of a CRC32C digest of every rank's shards, and the ranges."""
+    import torch
+
+    import isal_amd
+
+    T, W = args.total_stripes, d.world
+    first, count = isal_amd.partition(T, W, d.rank)
+    B = max(1, min(args.stripes, count))
+    dev = torch.device("cuda", d.gpu)
+    data = torch.empty((B, k, n), dtype=torch.uint8, device=dev)
+    data.random_(generator=torch.Generator(device=dev).manual_seed(1234 + d.rank))
+    out = torch.zeros((B, p, n), dtype=torch.uint8, device=dev)
+    tbls = isal_amd.ec_init_tables(k, p, a[k * k:])
+    dptr = [int(data[s, j].data_ptr()) for s in range(B) for j in range(k)]
+    cptr = [int(out[s, l].data_ptr()) for s in range(B) for l in range(p)]
+    full, rem = divmod(count, B)
+    batch = isal_amd.Batch(n, k, p, tbls, B, dptr, cptr)
+    rem_batch = isal_amd.Batch(n, k, p, tbls, rem, dptr[:rem * k], cptr[:rem * p]) if rem else None
+    stream = torch.cuda.current_stream(dev)
+    h = stream.cuda_stream
+    launches = full + (1 if rem else 0)
+
+    def step():
+        for _ in range(full):
+            batch.encode(h)
+        if rem_batch is not None:
+            rem_batch.encode(h)
+
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    d.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    d.barrier()
+    wall = d.max(t1 - t0)
+    step_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+
+    # self-check (all-ones Vandermonde row) and a digest of this rank's shards:
+    # CRC32C of every source and parity shard of the resident batch, summed
+    ok = True
+    for s_ in sorted({0, B // 2, B - 1}):
+        x = data[s_, 0].clone()
+        for j in range(1, k):
+            x ^= data[s_, j]
+        ok &= bool(torch.equal(x, out[s_, 0]))
+    crc = torch.zeros(B * (k + p), dtype=torch.int32, device=dev)
+    batch.crc(0xFFFFFFFF, crc, h)
+    torch.cuda.synchronize(dev)
+    digest = int((crc.to(torch.int64) & 0xFFFFFFFF).sum().item())
+    ranges = [0] * (2 * W)
+    ranges[2 * d.rank], ranges[2 * d.rank + 1] = first, count
+    red = d.sum_i64([count * args.steps, digest, 0 if ok else 1] + ranges)
+    encoded, digest_all, bad = red[0], red[1], red[2]
+    rng = [(red[3 + 2 * r], red[3 + 2 * r + 1]) for r in range(W)]
+    step_bytes = (k + p) * n * T
+    value = step_bytes * args.steps / wall / GIB
+    bytes_per_launch = (k + p) * n * count / launches if launches else 0
+    achieved = (k + p) * n * count / step_s / 1e9 if count else 0.0
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": W,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (uniform random bytes, torch RNG on device); each rank re-encodes its "
+                "resident batch for every stripe of its range",
+        "config": {
+            "workload": f"C5 encode: {T} stripes of k={k} p={p} Vandermonde RS, {n} B shards, split "
+                        f"over {W} GPU(s) in contiguous ranges, device-resident batches of {B}",
+            "k": k, "p": p, "shard_bytes": n, "total_stripes": T, "batch_stripes": B,
+            "stripe_ranges": [[f, f + c] for f, c in rng],
+            "parallelism": f"stripe ranges over {W} GPU(s), no data-path collective",
+        },
+        "per_gpu_gib_s": round(value / W, 2),
+        "stripes_encoded": encoded,
+        "stripes_expected": T * args.steps,
+        "shard_crc32c_digest": digest_all,
+        "self_check": bad == 0 and encoded == T * args.steps,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": f"ec_encode_v16<{p}, EncPol<{enc_group(k)}, 2, 2, 0>>",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "launch_ms": round(step_s / max(1, launches) * 1e3, 4),
+            "bytes_per_launch": int(bytes_per_launch),
+        },
+        "cpu_baseline": None,
+    }
+    if d.rank == 0:
+        print(json.dumps(result), flush=True)
+    batch.close()
+    if rem_batch is not None:
+        rem_batch.close()
+    d.close()
+    return 0
 
 
 # ---------------------------------------------------------------------------
@@ -361,6 +581,10 @@ def main(argv=None):
     a = np.frombuffer(control_plane_matrix(d, k, p), dtype=np.uint8)
     if args.workload.startswith("e2e"):
         return e2e(args, d, a, k, p, n)
+    if args.total_stripes:
+        if args.workload != "encode":
+            raise SystemExit("--total-stripes is the C5 encode configuration")
+        return total_stripes_run(args, d, a, k, p, n)
 
     # shards resident in HBM: data[s][j], coding[s][l]
     data = torch.empty((S, k, n), dtype=torch.uint8, device=dev)
@@ -575,18 +799,34 @@ def main(argv=None):
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        check = None
-        if args.workload in ("encode", "encode-crc", "encode-crc64"):
-            check = (data[0].cpu().numpy(), out[0].cpu().numpy())
-        with_crc = "crc64" if args.workload in ("crc64", "encode-crc64") else args.workload in ("encode-crc", "crc")
-        only_crc = args.workload in ("crc", "crc64")
-        result["cpu_baseline"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check, crc=with_crc,
-                                              encode=not only_crc)
-        # the reference's fast x86 path cannot be assembled here (no nasm): its
-        # AVX-512+GFNI kernels restated in C intrinsics, timed the same way
-        if args.workload not in ("crc64", "encode-crc64"):  # no SIMD port of the crc64 kernels
-            result["cpu_baseline_simd_port"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check,
-                                                            impl="gfni", crc=with_crc, encode=not only_crc)
+        if args.workload in ("encode", "decode", "update"):
+            # the reference's own perf harness (erasure_code_perf.c /
+            # erasure_code_update_perf.c) on this host's cores
+            result["cpu_baseline"] = ref_harness_baseline(args.workload, k, p, n, threads)
+            if args.workload == "encode":
+                result["cpu_parity_stripe_match"] = ref_parity_check(
+                    k, p, n, a[k * k:], data[0].cpu().numpy(), out[0].cpu().numpy())
+            elif args.workload == "decode":
+                result["cpu_parity_stripe_match"] = ref_parity_check(
+                    k, rows, n, c, [frag(0, i).cpu().numpy() for i in surv], out[0].cpu().numpy())
+            if args.workload in ("encode", "decode"):
+                # the reference's fast x86 path (AVX-512+GFNI, gf_Nvect_dot_prod_avx512_gfni)
+                # restated in C intrinsics: cache-warm like the reference harness, and
+                # cold (each thread cycling over distinct stripes, HBM-like streaming)
+                for key, ring in (("cpu_baseline_simd_port", 1), ("cpu_baseline_simd_port_cold", args.cold_ring)):
+                    result[key] = cpu_baseline(k, rows, n, min(args.cpu_seconds, 5.0), threads, None,
+                                               impl="gfni", ring=ring)
+        else:
+            check = None
+            if args.workload in ("encode-crc", "encode-crc64"):
+                check = (data[0].cpu().numpy(), out[0].cpu().numpy())
+            with_crc = "crc64" if args.workload in ("crc64", "encode-crc64") else args.workload in ("encode-crc", "crc")
+            only_crc = args.workload in ("crc", "crc64")
+            result["cpu_baseline"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check, crc=with_crc,
+                                                  encode=not only_crc)
+            if args.workload not in ("crc64", "encode-crc64"):  # no SIMD port of the crc64 kernels
+                result["cpu_baseline_simd_port"] = cpu_baseline(k, p, n, args.cpu_seconds, threads, check,
+                                                                impl="gfni", crc=with_crc, encode=not only_crc)
     else:
         result["cpu_baseline"] = None
     if d.rank == 0:
@@ -606,7 +846,7 @@ def e2e(args, d: Dist, a, k, p, n):
     import isal_amd
 
     mode = "update" if args.workload == "e2e-update" else "encode"
-    ring = max(2 * args.depth, 4)
+    ring = args.ring or max(2 * args.depth, 4)
     src = torch.empty((ring, k, n), dtype=torch.uint8).pin_memory()
     src.random_(generator=torch.Generator().manual_seed(5 + d.rank))
     par = torch.empty((ring, p, n), dtype=torch.uint8).pin_memory()
@@ -642,7 +882,8 @@ def e2e(args, d: Dist, a, k, p, n):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (uniform random bytes, pinned host memory)",
-        "config": {"workload": f"{mode} pipeline, k={k} p={p}, {n} B shards, depth {args.depth}",
+        "config": {"workload": f"{mode} pipeline, k={k} p={p}, {n} B shards, depth {args.depth}, "
+                               f"{ring} pinned host stripes cycled",
                    "k": k, "p": p, "shard_bytes": n},
         "pcie": {"h2d_gb_s": round(k * n * args.steps / wall / 1e9, 2),
                  "d2h_gb_s": round(p * n * args.steps / wall / 1e9, 2),
@@ -658,7 +899,10 @@ def e2e(args, d: Dist, a, k, p, n):
 
 
 def dry_run(args, d: Dist):
-    """Harness only (CPU, gloo): control-plane broadcast, barrier, max-over-ranks."""
+    """Harness only (CPU, gloo): control-plane broadcast, barrier, max-over-ranks,
+    and — with --total-stripes — the C5 partition of the stripes over the
+    ranks (isal_hip_multi_partition, the library's pure host function) with
+    the SUM all-reduce of counts and ranges that the GPU run performs."""
     import numpy as np
 
     k, p = args.k, args.p
@@ -666,10 +910,22 @@ def dry_run(args, d: Dist):
     sleep = 0.002 * (1 + d.rank)
     wall = timed_steps(d, lambda: time.sleep(sleep), lambda: None, args.steps, args.warmup)
     total_stripes = d.sum(float(args.stripes))
+    out = {"metric": METRIC, "dry_run": True, "n_gpus": d.world, "wall": wall, "stripes": total_stripes,
+           "matrix_fnv": int(np.frombuffer(a, np.uint8).sum())}
+    if args.total_stripes:
+        import isal_amd
+
+        first, count = isal_amd.partition(args.total_stripes, d.world, d.rank)
+        B = max(1, min(args.stripes, count))
+        launches = count // B + (1 if count % B else 0)
+        ranges = [0] * (2 * d.world)
+        ranges[2 * d.rank], ranges[2 * d.rank + 1] = first, count
+        red = d.sum_i64([count * args.steps, launches] + ranges)
+        out.update({"stripes_encoded": red[0], "stripes_expected": args.total_stripes * args.steps,
+                    "launches_per_step": red[1],
+                    "stripe_ranges": [[red[2 + 2 * r], red[2 + 2 * r] + red[3 + 2 * r]] for r in range(d.world)]})
     if d.rank == 0:
-        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": d.world,
-                          "wall": wall, "stripes": total_stripes,
-                          "matrix_fnv": int(np.frombuffer(a, np.uint8).sum())}), flush=True)
+        print(json.dumps(out), flush=True)
     d.close()
     return 0
 

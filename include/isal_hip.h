@@ -135,6 +135,33 @@ int isal_hip_pipe_flush(isal_hip_pipe *p);
 
 int isal_hip_pipe_destroy(isal_hip_pipe *p);
 
+/* ---- several GPUs from one process ---------------------------------------- */
+
+/*
+ * Host-resident stripes encoded on ndev GPUs at once (0 = every visible GPU).
+ * A call's stripes are split into contiguous, balanced ranges
+ * (isal_hip_multi_partition); GPU d streams its range through its own
+ * pipeline (as isal_hip_pipe, mode ENCODE) on its own host thread, so the
+ * GPUs never exchange data. isal_hip_multi_encode blocks until every parity
+ * shard is in host memory; data[s*k + j] / coding[s*rows + l] are host
+ * pointers (pinned for full copy/compute overlap). Callers whose shards are
+ * already in each GPU's HBM use one isal_hip_batch per device instead.
+ */
+typedef struct isal_hip_multi isal_hip_multi;
+
+int isal_hip_multi_create(isal_hip_multi **out, int ndev, int len, int k, int rows,
+                          const unsigned char *gftbls, int depth);
+int isal_hip_multi_ndev(const isal_hip_multi *m);
+int isal_hip_multi_encode(isal_hip_multi *m, long long nstripes, unsigned char *const *data,
+                          unsigned char *const *coding);
+int isal_hip_multi_destroy(isal_hip_multi *m);
+
+/* Stripes [*first, *first + *count) of nstripes belong to device (or rank)
+ * dev of ndev: contiguous, covering, sizes differ by at most one. Pure
+ * arithmetic, no GPU needed. */
+void isal_hip_multi_partition(long long nstripes, int ndev, int dev, long long *first,
+                              long long *count);
+
 /* ---- routing of the drop-in calls and configuration --------------------- */
 
 /*

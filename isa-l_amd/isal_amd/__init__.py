@@ -27,7 +27,7 @@ __all__ = [
     "ec_encode_data_base", "ec_encode_data_update", "ec_encode_data_update_base",
     "gf_vect_dot_prod", "gf_vect_dot_prod_base", "gf_vect_mad", "gf_vect_mad_base",
     "gf_vect_mul", "gf_vect_mul_base", "Batch", "Pipe", "kernel_launches", "max_rows_per_pass",
-    "version", "addr", "cpu_calls", "fallbacks", "reload_config",
+    "version", "addr", "cpu_calls", "fallbacks", "reload_config", "Multi", "partition",
 ]
 
 LIB_PATH = os.environ.get(
@@ -110,6 +110,12 @@ def lib() -> ctypes.CDLL:
             "isal_hip_pipe_destroy": (i, [ctypes.c_void_p]),
             "isal_hip_kernel_launches": (ctypes.c_ulonglong, []),
             "isal_hip_cpu_calls": (ctypes.c_ulonglong, []),
+            "isal_hip_multi_create": (i, [ctypes.POINTER(ctypes.c_void_p), i, i, i, i, _u8p, i]),
+            "isal_hip_multi_ndev": (i, [ctypes.c_void_p]),
+            "isal_hip_multi_encode": (i, [ctypes.c_void_p, ctypes.c_longlong, _u8pp, _u8pp]),
+            "isal_hip_multi_destroy": (i, [ctypes.c_void_p]),
+            "isal_hip_multi_partition": (None, [ctypes.c_longlong, i, i, ctypes.POINTER(ctypes.c_longlong),
+                                                ctypes.POINTER(ctypes.c_longlong)]),
             "isal_hip_fallbacks": (ctypes.c_ulonglong, []),
             "isal_hip_config_reload": (None, []),
             "isal_hip_max_rows_per_pass": (i, []),
@@ -375,6 +381,51 @@ class Pipe:
             self.close()
         except Exception:
             pass
+
+
+class Multi:
+    """Host-resident stripes encoded on several GPUs of this process
+    (include/isal_hip.h multi-device): contiguous stripe ranges per GPU, one
+    pipeline and host thread each. ndev = 0: every visible GPU."""
+
+    def __init__(self, len_: int, k: int, rows: int, gftbls, ndev: int = 0, depth: int = 3):
+        self.len, self.k, self.rows = len_, k, rows
+        h = ctypes.c_void_p()
+        rc = lib().isal_hip_multi_create(ctypes.byref(h), ndev, len_, k, rows, _p(gftbls), depth)
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_multi_create failed ({rc})")
+        self._h = h
+
+    @property
+    def ndev(self) -> int:
+        return int(lib().isal_hip_multi_ndev(self._h))
+
+    def encode(self, nstripes: int, data: Sequence, coding: Sequence) -> None:
+        """data[s*k + j], coding[s*rows + l]: host buffers of stripe s."""
+        if len(data) != nstripes * self.k or len(coding) != nstripes * self.rows:
+            raise ValueError("pointer lists must hold nstripes*k and nstripes*rows entries")
+        rc = lib().isal_hip_multi_encode(self._h, nstripes, _pp(data), _pp(coding))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_multi_encode failed ({rc})")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().isal_hip_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def partition(nstripes: int, ndev: int, dev: int) -> tuple[int, int]:
+    """(first, count) of device/rank `dev`'s contiguous stripe range
+    (isal_hip_multi_partition; no GPU needed)."""
+    first, count = ctypes.c_longlong(), ctypes.c_longlong()
+    lib().isal_hip_multi_partition(nstripes, ndev, dev, ctypes.byref(first), ctypes.byref(count))
+    return int(first.value), int(count.value)
 
 
 def kernel_launches() -> int:

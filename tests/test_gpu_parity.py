@@ -1108,3 +1108,39 @@ def test_bench_two_ranks_on_one_gpu(gpu):
         assert len(lines) == 1, r.stdout
         out = json.loads(lines[0])
         assert out["n_gpus"] == 2 and out["value"] > 0 and out["self_check"] is True, out
+    # C5 mode: 300 stripes split over the two ranks, batches of 64 (4 full + 1 ragged
+    # launch per rank), every stripe counted once per step
+    r = subprocess.run(cmd + ["--total-stripes", "300"], capture_output=True, text=True, timeout=600,
+                       cwd=ecutil.REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["config"]["stripe_ranges"] == [[0, 150], [150, 300]], out
+    assert out["stripes_encoded"] == 300 * 4 and out["self_check"] is True, out
+    assert out["scaling"] == "strong" and out["value"] > 0
+
+
+def test_multi_device_encode_host_stripes_vs_oracle(engine, oracle, gpu):
+    """isal_hip_multi_*: host stripes over every visible GPU (here: one), each
+    GPU its contiguous range through its own pipeline; == oracle."""
+    import torch
+
+    k, p, n, ns = 10, 4, 65536 + 32, 9
+    a = engine.gf_gen_rs_matrix(k + p, k)
+    tbls = engine.ec_init_tables(k, p, a[k * k:])
+    src = torch.empty((ns, k, n), dtype=torch.uint8).pin_memory()
+    src.random_(generator=torch.Generator().manual_seed(9))
+    par = torch.full((ns, p, n), 0xEE, dtype=torch.uint8).pin_memory()
+    m = engine.Multi(n, k, p, tbls, ndev=0, depth=2)
+    assert m.ndev == torch.cuda.device_count()
+    launches = engine.kernel_launches()
+    m.encode(ns, [src[s, j] for s in range(ns) for j in range(k)], [par[s, l] for s in range(ns) for l in range(p)])
+    assert engine.kernel_launches() >= launches + ns
+    h = src.numpy()
+    want = _oracle_encode_all(oracle, a[k * k:], k, p, [[h[s, j] for j in range(k)] for s in range(ns)])
+    for s in range(ns):
+        for l in range(p):
+            assert np.array_equal(par[s, l].numpy(), want[s][l]), (s, l)
+    m.encode(0, [], [])
+    m.close()
+    with pytest.raises(RuntimeError):
+        engine.Multi(n, k, p, tbls, ndev=torch.cuda.device_count() + 1)

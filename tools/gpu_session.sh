@@ -30,7 +30,7 @@ run() {  # name seconds cmd...
 for s in $STEPS; do
         case $s in
         tests)
-                run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+                run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread
                 grep -E "PASSED|FAILED|SKIPPED|ERROR|passed|failed" "$OUT/pytest_gpu.log" > "$OUT/pytest_gpu_summary.txt" || true
                 ;;
         tests_crc)
@@ -138,6 +138,19 @@ for s in $STEPS; do
                 run pmc_fetch_$wl 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$wl" -o f -- python3 bench.py $args --no-cpu-baseline --steps 3 --warmup 1
                 run pmc_write_$wl 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$wl" -o w -- python3 bench.py $args --no-cpu-baseline --steps 3 --warmup 1
                 python3 tools/pmc_csv.py "$OUT/pmc_$wl.csv" "$cfg" "python bench.py $args --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_$wl" "$OUT/pmc_write_$wl" $kern
+                ;;
+        c5)
+                run bench_c5 600 python bench.py --total-stripes 1048576 --steps 2 --warmup 1
+                cp "$OUT/bench_c5.log" "$OUT/bench_c5.json"
+                ;;
+        route)
+                run route_crossover 300 python tools/route_crossover.py
+                run latency_probe 120 python tools/latency_probe.py
+                ;;
+        e2ering)
+                for dr in 2:4 2:12 6:6 6:12 3:3; do
+                        run bench_e2e_encode_d${dr%:*}_r${dr#*:} 300 python bench.py --workload e2e-encode --steps 200 --warmup 10 --depth ${dr%:*} --ring ${dr#*:}
+                done
                 ;;
         e2esweep)
                 for dp in ${E2E_DEPTHS:-2 3 4 6}; do
