@@ -225,14 +225,30 @@ CONFORMANCE = ["gf_inverse_test", "gf_vect_mul_test", "gf_vect_mul_base_test",
                "xor_gen_test", "pq_gen_test", "xor_check_test", "pq_check_test"]
 
 
-@pytest.mark.parametrize("name", CONFORMANCE)
-def test_reference_test_programs_on_cpu_route(name):
+def run_programs(directory, names, env, timeout=600):
+    """Run the reference's test programs concurrently (one per host core);
+    returns {name: (rc, output tail)}, skipping programs that are not built."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(name):
+        exe = os.path.join(directory, name)
+        if not os.path.exists(exe):
+            return name, None
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=timeout, env=env)
+        return name, (r.returncode, (r.stdout + r.stderr)[-2000:])
+
+    with ThreadPoolExecutor(max_workers=max(1, min(8, os.cpu_count() or 1))) as ex:
+        return dict(ex.map(one, names))
+
+
+def test_reference_test_programs_on_cpu_route():
     """The reference's own EC / RAID test programs, unmodified, linked against
     libisal_hip.so, with every call on the CPU route."""
-    exe = os.path.join(ecutil.REF_DIR, "conformance", name)
-    if not os.path.exists(exe):
-        pytest.skip(f"{name} not built (make -C oracle conformance needs /root/reference)")
-    env = dict(os.environ, ISAL_HIP_BACKEND="cpu")
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
-    assert "pass" in r.stdout.lower()
+    res = run_programs(os.path.join(ecutil.REF_DIR, "conformance"), CONFORMANCE,
+                       dict(os.environ, ISAL_HIP_BACKEND="cpu"))
+    if all(v is None for v in res.values()):
+        pytest.skip("not built (make -C oracle conformance needs /root/reference)")
+    for name, v in res.items():
+        assert v is not None, f"{name} not built"
+        rc, out = v
+        assert rc == 0 and "pass" in out.lower(), (name, out)
