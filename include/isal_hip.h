@@ -119,6 +119,8 @@ int isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long lo
  */
 #define ISAL_HIP_PIPE_UPDATE 0
 #define ISAL_HIP_PIPE_ENCODE 1
+/* depth is capped at this many stripes in flight (more only slows the copies) */
+#define ISAL_HIP_PIPE_MAX_DEPTH 4
 
 typedef struct isal_hip_pipe isal_hip_pipe;
 
@@ -170,7 +172,7 @@ void isal_hip_multi_partition(long long nstripes, int ndev, int dev, long long *
  *   - any device-resident shard: the GPU kernels;
  *   - host-resident shards, (k + rows) * len > ISAL_HIP_CPU_MAX_BYTES: the GPU
  *     kernels through pinned / HBM staging;
- *   - host-resident shards up to ISAL_HIP_CPU_MAX_BYTES (default 1 MiB), or a
+ *   - host-resident shards up to ISAL_HIP_CPU_MAX_BYTES (default 8 MiB), or a
  *     host without a usable GPU: the engine's CPU route.
  * ISAL_HIP_BACKEND=gpu forces the kernels for every call (and aborts when no
  * GPU is usable), =cpu sends every host-resident call to the CPU route,

@@ -132,7 +132,7 @@ backend(void)
  * route under ISAL_HIP_BACKEND=auto (override: ISAL_HIP_CPU_MAX_BYTES). Below
  * it the ~30 us GPU round trip costs more than the arithmetic (DESIGN.md §3,
  * measured crossover in profiles/r02_route_crossover.txt). */
-#define DEFAULT_CPU_MAX_BYTES ((size_t) 1 << 20)
+#define DEFAULT_CPU_MAX_BYTES ((size_t) 8 << 20)
 
 static size_t
 cpu_max_bytes(void)

@@ -147,6 +147,11 @@ for s in $STEPS; do
                 run route_crossover 300 python tools/route_crossover.py
                 run latency_probe 120 python tools/latency_probe.py
                 ;;
+        e2etrace)
+                for dp in 2 6; do
+                        run e2etrace_d$dp 300 rocprofv3 --memory-copy-trace --kernel-trace --stats --output-format csv -d "$OUT/e2etrace_d$dp" -o t -- python3 bench.py --workload e2e-encode --steps 100 --warmup 10 --depth $dp
+                done
+                ;;
         e2ering)
                 for dr in 2:4 2:12 6:6 6:12 3:3; do
                         run bench_e2e_encode_d${dr%:*}_r${dr#*:} 300 python bench.py --workload e2e-encode --steps 200 --warmup 10 --depth ${dr%:*} --ring ${dr#*:}
