@@ -636,7 +636,7 @@ def main(argv=None):
             if args.workload == "encode-crc":
                 u = enc_group(k)  # one load group (k == U): source CRC chains in registers
                 reg = k == u and os.environ.get("ISAL_HIP_CRC_SRC_CHAIN", "reg") != "lds"
-                kernel = f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true>"
+                kernel = f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true, true>"
                 workload = (f"C2 encode + CRC32C (crc32_iscsi) of all k+p shards in one pass: k={k} "
                             f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
             else:
@@ -650,7 +650,7 @@ def main(argv=None):
             bytes_per_launch = (k + p) * n * S
             u = enc_group(k)
             reg = k == u and os.environ.get("ISAL_HIP_CRC64_SRC_CHAIN") == "reg"
-            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(reg).lower()}>"
+            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(reg).lower()}, true>"  # X0: Vandermonde row 0 derived
             workload = (f"C2 encode + CRC64 (crc64_ecma_refl) of all k+p shards in one pass: k={k} "
                         f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
         elif args.workload == "crc64":

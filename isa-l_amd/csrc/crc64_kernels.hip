@@ -55,25 +55,73 @@ __device__ __forceinline__ void field_offsets8(uint32_t w, uint32_t (&o)[kF]) {
   o[6] = (w >> 27) & 0x18u;
 }
 
-// XOR of the 7 field lookups of w in the 7 consecutive 32-entry tables at t.
-__device__ __forceinline__ uint64_t lookup7(const uint64_t* t, uint32_t w) {
-  uint32_t o[kF];
-  field_offsets8(w, o);
-  const char* b = reinterpret_cast<const char*>(t);
-  auto at = [&](int f) { return *reinterpret_cast<const uint64_t*>(b + f * 256 + o[f]); };
-  return at(0) ^ at(1) ^ at(2) ^ at(3) ^ at(4) ^ at(5) ^ at(6);
+// 64-bit XOR accumulator kept as two dwords so that every fold is one
+// v_bitop3 (3-input XOR) per half: a lookup costs one XOR op instead of two
+// (the compiler does not form bitop3 from 64-bit XOR chains by itself).
+struct X64 {
+  uint32_t lo, hi;
+  __device__ __forceinline__ void add2(uint64_t x, uint64_t y) {
+    lo = xor3(lo, static_cast<uint32_t>(x), static_cast<uint32_t>(y));
+    hi = xor3(hi, static_cast<uint32_t>(x >> 32), static_cast<uint32_t>(y >> 32));
+  }
+  __device__ __forceinline__ void add(uint64_t x) {
+    lo ^= static_cast<uint32_t>(x);
+    hi ^= static_cast<uint32_t>(x >> 32);
+  }
+  __device__ __forceinline__ uint64_t get() const {
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+  }
+};
+
+__device__ __forceinline__ X64 x64(uint64_t v) {
+  return {static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32)};
 }
 
-// M(v) for a map stored as 14 field tables.
+// Entry of field f of table set t at byte offset o (field tables are 256 B apart).
+__device__ __forceinline__ uint64_t tab_at(const uint64_t* t, int f, uint32_t o) {
+  return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(t) + f * 256 + o);
+}
+
+// acc ^= the 14 field lookups of the two dwords (w0, w1) in the 14 consecutive
+// 32-entry tables at t: seven 3-input XORs per half.
+__device__ __forceinline__ void lookup14(X64& acc, const uint64_t* t, uint32_t w0, uint32_t w1) {
+  uint32_t o[kF], q[kF];
+  field_offsets8(w0, o);
+  field_offsets8(w1, q);
+  const uint64_t* u = t + kF * 32;
+  acc.add2(tab_at(t, 0, o[0]), tab_at(t, 1, o[1]));
+  acc.add2(tab_at(t, 2, o[2]), tab_at(t, 3, o[3]));
+  acc.add2(tab_at(t, 4, o[4]), tab_at(t, 5, o[5]));
+  acc.add2(tab_at(t, 6, o[6]), tab_at(u, 0, q[0]));
+  acc.add2(tab_at(u, 1, q[1]), tab_at(u, 2, q[2]));
+  acc.add2(tab_at(u, 3, q[3]), tab_at(u, 4, q[4]));
+  acc.add2(tab_at(u, 5, q[5]), tab_at(u, 6, q[6]));
+}
+
+// acc ^= M(v) for a map stored as 14 field tables.
+__device__ __forceinline__ void apply_op_acc(X64& acc, const uint64_t* op, uint64_t v) {
+  lookup14(acc, op, static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
+}
+
 __device__ __forceinline__ uint64_t apply_op(const uint64_t* op, uint64_t v) {
-  return lookup7(op, static_cast<uint32_t>(v)) ^ lookup7(op + kF * 32, static_cast<uint32_t>(v >> 32));
+  X64 a{0u, 0u};
+  apply_op_acc(a, op, v);
+  return a.get();
 }
 
-// raw(0, 16-byte chunk), dwords little-endian.
+// acc ^= raw(0, 16-byte chunk) through the chunk map at t, dwords little-endian.
+__device__ __forceinline__ void chunk_acc(X64& acc, const uint64_t* t, uint32_t w0, uint32_t w1,
+                                          uint32_t w2, uint32_t w3) {
+  constexpr int D = kF * 32;
+  lookup14(acc, t, w0, w1);
+  lookup14(acc, t + 2 * D, w2, w3);
+}
+
 __device__ __forceinline__ uint64_t chunk_crc(const uint64_t* t, uint32_t w0, uint32_t w1,
                                               uint32_t w2, uint32_t w3) {
-  constexpr int D = kF * 32;
-  return (lookup7(t, w0) ^ lookup7(t + D, w1)) ^ (lookup7(t + 2 * D, w2) ^ lookup7(t + 3 * D, w3));
+  X64 a{0u, 0u};
+  chunk_acc(a, t, w0, w1, w2, w3);
+  return a.get();
 }
 
 __device__ __forceinline__ uint32_t le32(const uint8_t* p) {
@@ -146,17 +194,21 @@ __global__ __launch_bounds__(kBlock) void crc64_shards(const uint64_t* __restric
           x[g] = load16<kBufNT>(base, static_cast<long long>(t + g) * kTile + lane, len);
 #pragma unroll
         for (unsigned g = 0; g < B; g += M) {
-          uint64_t c = 0;
+          X64 c{0u, 0u};
 #pragma unroll
           for (int h = 0; h < M; ++h)
-            c ^= chunk_crc(chunk_map<M>(lt, M - 1 - h), x[g + h].x, x[g + h].y, x[g + h].z,
-                           x[g + h].w);
-          a = apply_op(shift_m, a) ^ c;
+            chunk_acc(c, chunk_map<M>(lt, M - 1 - h), x[g + h].x, x[g + h].y, x[g + h].z,
+                      x[g + h].w);
+          apply_op_acc(c, shift_m, a);
+          a = c.get();
         }
       }
       for (; t < t1; ++t) {
         const uint4 x = load16<kBufNT>(base, static_cast<long long>(t) * kTile + lane, len);
-        a = apply_op(lt + kShift, a) ^ chunk_crc(lt + kChunk, x.x, x.y, x.z, x.w);
+        X64 c{0u, 0u};
+        chunk_acc(c, lt + kChunk, x.x, x.y, x.z, x.w);
+        apply_op_acc(c, lt + kShift, a);
+        a = c.get();
       }
     } else {
       for (; t < t1; ++t)
@@ -188,11 +240,15 @@ __device__ __forceinline__ uint64_t lane_tree(uint64_t* red, const uint64_t* tre
 //      the tree, so lane q-1's chunk is the last one;
 //  s = Z^(16q)(X) ^ T, then the last tail % 16 bytes one at a time;
 //  crc64 = ~(Z^len(~init) ^ s).
+// x0_src != 0: shard x0_shard of every stripe (parity row 0 of a fused X0
+// encode) has no partials of its own; they are the XOR of the partials of the
+// sources in x0_src. (Its ragged tail is read from the shard like any other.)
 template <bool REFL>
 __global__ __launch_bounds__(kBlock) void crc64_combine(
     const uint64_t* __restrict__ part, const uint64_t* __restrict__ ptrs, int ptr_stride, int nsh,
     int len, unsigned nblk, unsigned nfull, const uint64_t* __restrict__ tabs, uint64_t init_term,
-    uint64_t* __restrict__ out, unsigned nshard_total) {
+    uint64_t* __restrict__ out, unsigned nshard_total, unsigned x0_shard,
+    unsigned long long x0_src) {
   __shared__ uint64_t lt[ISAL_HIP_CRC64_COMBINE_ENTRIES];
   __shared__ uint64_t red[kBlock];
   load_lds<ISAL_HIP_CRC64_COMBINE_ENTRIES>(lt, tabs);
@@ -205,10 +261,19 @@ __global__ __launch_bounds__(kBlock) void crc64_combine(
     uint64_t x = 0, tq = 0;
     if (nblk) {
       const uint64_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + threadIdx.x;
+      const uint64_t* ps = part + static_cast<size_t>(stripe) * nsh * nblk * kBlock + threadIdx.x;
+      const bool derived = x0_src && i == x0_shard;
       uint64_t h = 0;
-      for (unsigned b = 0; b < nblk; ++b)
-        h = apply_op(lt + (b + 1 == nblk ? ISAL_HIP_CRC64_OP_LAST : ISAL_HIP_CRC64_OP_BLOCK), h) ^
-            pp[static_cast<size_t>(b) * kBlock];
+      for (unsigned b = 0; b < nblk; ++b) {
+        uint64_t v = 0;
+        if (!derived) {
+          v = pp[static_cast<size_t>(b) * kBlock];
+        } else {
+          for (unsigned j = 0; j < x0_shard; ++j)
+            if ((x0_src >> j) & 1ull) v ^= ps[(static_cast<size_t>(j) * nblk + b) * kBlock];
+        }
+        h = apply_op(lt + (b + 1 == nblk ? ISAL_HIP_CRC64_OP_LAST : ISAL_HIP_CRC64_OP_BLOCK), h) ^ v;
+      }
       red[threadIdx.x] = h;
       __syncthreads();
       x = lane_tree(red, lt + ISAL_HIP_CRC64_OP_TREE);
@@ -303,11 +368,10 @@ constexpr int kT1 = kKernTab, kZ2 = kKernTab + kCE;
 template <int PH>
 __device__ __forceinline__ uint64_t chain_step(const uint64_t* lt, uint64_t a, uint32_t w0,
                                                uint32_t w1, uint32_t w2, uint32_t w3) {
-  const uint64_t c = chunk_crc(lt + (PH == 1 ? kT1 : kChunk), w0, w1, w2, w3);
-  if constexpr (PH == 2)
-    return a ^ c;
-  else
-    return apply_op(lt + (PH == 1 ? kZ2 : kShift), a) ^ c;
+  X64 c = PH == 2 ? x64(a) : X64{0u, 0u};
+  chunk_acc(c, lt + (PH == 1 ? kT1 : kChunk), w0, w1, w2, w3);
+  if constexpr (PH != 2) apply_op_acc(c, lt + (PH == 1 ? kZ2 : kShift), a);
+  return c.get();
 }
 
 template <int P, int U, bool REG>
@@ -317,7 +381,12 @@ constexpr int fused64_waves() {
   return w > 8 ? 8 : (w < 2 ? 2 : w);
 }
 
-template <int P, int U, bool REG>
+// X0: parity row 0 has only 0/1 coefficients (RS Vandermonde row 0, RAID P):
+// it is the XOR of some sources, so its chain is not computed and
+// crc64_combine derives its partials from those sources' (CRC is
+// GF(2)-linear). A compile-time variant: a runtime row mask in the tile loop
+// costs registers.
+template <int P, int U, bool REG, bool X0 = false>
 __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encode_crc64_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, const uint32_t* __restrict__ tbl, int len,
     int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged, int pair,
@@ -372,7 +441,8 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
 #pragma unroll
       for (int l = 0; l < P; ++l) {
         store16<kNT>(sp[k + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
-        ao[l] = chain_step<PH>(lt, ao[l], acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+        if (!(X0 && l == 0))
+          ao[l] = chain_step<PH>(lt, ao[l], acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
       }
     };
     if constexpr (REG) {
@@ -442,7 +512,7 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
       for (int j = 0; j < k; ++j) pp[j * sstep] = la[j * kBlock + threadIdx.x];
     }
 #pragma unroll
-    for (int l = 0; l < P; ++l) pp[(k + l) * sstep] = ao[l];
+    for (int l = X0 ? 1 : 0; l < P; ++l) pp[(k + l) * sstep] = ao[l];
   }
 }
 
@@ -476,46 +546,51 @@ bool src_chain_reg64() {
 template <int P, int U>
 void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
                     const uint32_t* tbl, int len, int k, unsigned nitems,
-                    const isal_hip_crc64_geom& g, const uint64_t* tabs, uint64_t* part) {
+                    const isal_hip_crc64_geom& g, const isal_hip_xrows& xr, const uint64_t* tabs,
+                    uint64_t* part) {
   const int ragged = g.tail != 0;
-  if (k == U && src_chain_reg64())
-    hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, true>), dim3(grid), dim3(kBlock), 0, s, ptrs,
-                       ptr_stride, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),
-                       static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), ragged, pair_step(),
-                       tabs, part);
-  else
-    hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, false>), dim3(grid), dim3(kBlock),
-                       static_cast<size_t>(k) * kBlock * 8, s, ptrs, ptr_stride, tbl, len, k, nitems,
-                       static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
-                       static_cast<unsigned>(g.nfull), ragged, pair_step(), tabs, part);
+#define FUSED64_LAUNCH(REG, X0, LDS)                                                              \
+  hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, REG, X0>), dim3(grid), dim3(kBlock), LDS, s, ptrs, \
+                     ptr_stride, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),             \
+                     static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), ragged,         \
+                     pair_step(), tabs, part)
+  const size_t lds = static_cast<size_t>(k) * kBlock * 8;
+  if (k == U && src_chain_reg64()) {
+    if (xr.rows & 1u) FUSED64_LAUNCH(true, true, 0); else FUSED64_LAUNCH(true, false, 0);
+  } else {
+    if (xr.rows & 1u) FUSED64_LAUNCH(false, true, lds); else FUSED64_LAUNCH(false, false, lds);
+  }
+#undef FUSED64_LAUNCH
 }
 
 template <int P>
 void fused64_pass(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
                   const uint32_t* tbl, int len, int k, unsigned nitems,
-                  const isal_hip_crc64_geom& g, const uint64_t* tabs, uint64_t* part) {
+                  const isal_hip_crc64_geom& g, const isal_hip_xrows& xr, const uint64_t* tabs,
+                  uint64_t* part) {
   switch (group_u(k)) {
 #define FUSED64_U(u) \
-  case u: launch_fused64<P, u>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, tabs, part); break;
+  case u: launch_fused64<P, u>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, xr, tabs, part); break;
     FUSED64_U(12) FUSED64_U(10) FUSED64_U(8) FUSED64_U(6) FUSED64_U(5)
 #undef FUSED64_U
-    default: launch_fused64<P, 4>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, tabs, part);
+    default: launch_fused64<P, 4>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, xr, tabs, part);
   }
 }
 
 int launch_combine64(const uint64_t* part, const uint64_t* ptrs, int ptr_stride, int nsh, int len,
                      const isal_hip_crc64_geom& g, int refl, const uint64_t* tabs,
-                     uint64_t init_term, uint64_t* out, unsigned nshard, hipStream_t s) {
+                     uint64_t init_term, uint64_t* out, unsigned nshard, hipStream_t s,
+                     unsigned x0_shard = 0, unsigned long long x0_src = 0) {
   // each combine workgroup copies the 52 KB table set once: cap the grid
   const unsigned grid = nshard < 2048 ? nshard : 2048;
   if (refl)
     hipLaunchKernelGGL(crc64_combine<true>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
                        nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
-                       tabs, init_term, out, nshard);
+                       tabs, init_term, out, nshard, x0_shard, x0_src);
   else
     hipLaunchKernelGGL(crc64_combine<false>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
                        nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
-                       tabs, init_term, out, nshard);
+                       tabs, init_term, out, nshard, x0_shard, x0_src);
   isal_hip_count_launch();
   return static_cast<int>(hipGetLastError());
 }
@@ -566,10 +641,12 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
 
 extern "C" int isal_hip_launch_encode_crc64(const uint64_t* d_ptrs, int k, int rows,
                                             long long nstripes, int len, const uint32_t* d_tbl,
-                                            int refl, int tt, const uint64_t* d_tabs,
-                                            uint64_t* d_part, uint64_t init_term, uint64_t* out,
-                                            void* stream) {
+                                            const isal_hip_xrows* xrp, int refl, int tt,
+                                            const uint64_t* d_tabs, uint64_t* d_part,
+                                            uint64_t init_term, uint64_t* out, void* stream) {
   if (nstripes <= 0) return 0;
+  isal_hip_xrows xr{};
+  if (xrp) xr = *xrp;
   isal_hip_crc64_geom g;
   isal_hip_crc64_geometry(len, tt, &g);
   if (len % kVec || g.nblk == 0 || rows < 1 || rows > EC_MAX_ROWS_PER_PASS || k < 1 ||
@@ -586,7 +663,7 @@ extern "C" int isal_hip_launch_encode_crc64(const uint64_t* d_ptrs, int k, int r
     uint64_t* part = d_part + static_cast<size_t>(s0) * nsh * g.nblk * kBlock;
     switch (rows) {
 #define FUSED64_P(p) \
-  case p: fused64_pass<p>(nitems, s, ptrs, nsh, d_tbl, len, k, nitems, g, d_tabs, part); break;
+  case p: fused64_pass<p>(nitems, s, ptrs, nsh, d_tbl, len, k, nitems, g, xr, d_tabs, part); break;
       FUSED64_P(1) FUSED64_P(2) FUSED64_P(3) FUSED64_P(4) FUSED64_P(5) FUSED64_P(6) FUSED64_P(7)
       FUSED64_P(8)
 #undef FUSED64_P
@@ -595,7 +672,8 @@ extern "C" int isal_hip_launch_encode_crc64(const uint64_t* d_ptrs, int k, int r
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);
     const int r = launch_combine64(part, ptrs, nsh, nsh, len, g, refl, d_tabs, init_term,
-                                   out + s0 * nsh, static_cast<unsigned>(ns * nsh), s);
+                                   out + s0 * nsh, static_cast<unsigned>(ns * nsh), s,
+                                   static_cast<unsigned>(k), (xr.rows & 1u) ? xr.src[0] : 0ull);
     if (r) return r;
   }
   return 0;

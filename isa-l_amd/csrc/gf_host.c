@@ -227,6 +227,28 @@ isal_hip_build_tables(int k, int rows, const unsigned char *gftbls, uint32_t *tb
         }
 }
 
+void
+isal_hip_xor_rows(int k, int rows, const unsigned char *gftbls, isal_hip_xrows *x)
+{
+        int l, j;
+        memset(x, 0, sizeof(*x));
+        if (k < 1 || k > 64 || isal_hip_knob(ISAL_HIP_KNOB_CRC_XROWS) == 0)
+                return;
+        for (l = 0; l < rows && l < EC_MAX_ROWS_PER_PASS; l++) {
+                unsigned long long m = 0;
+                for (j = 0; j < k; j++) {
+                        const unsigned char c = gftbls[((size_t) l * k + j) * 32 + 1];
+                        if (c > 1)
+                                break;
+                        m |= (unsigned long long) c << j;
+                }
+                if (j == k) {
+                        x->rows |= 1u << l;
+                        x->src[l] = m;
+                }
+        }
+}
+
 /* ---- version (reference isal_api.h:93,104) ------------------------------ */
 
 const char *

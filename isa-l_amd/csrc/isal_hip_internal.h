@@ -71,6 +71,19 @@ unsigned long long isal_hip_run(int op, int len, int k, int rows, int vec_i,
                                 const unsigned char *gftbls, unsigned char *const *src, int nsrc,
                                 unsigned char *const *dst);
 
+/* Parity rows of a pass whose coefficients are all 0 or 1 (RS Vandermonde row
+ * 0, RAID P): such a row is the XOR of some sources, so — CRC being
+ * GF(2)-linear in the data — its raw CRC partials are the XOR of those
+ * sources' partials. The fused encode+CRC kernels skip checksumming row 0 when
+ * it is such a row (bit 0 of rows; a compile-time kernel variant) and the
+ * combine kernels derive it. rows: bit l set for such a row l <
+ * EC_MAX_ROWS_PER_PASS (k <= 64); src[l]: bit j set where c[l][j] == 1. */
+typedef struct {
+        unsigned rows;
+        unsigned long long src[EC_MAX_ROWS_PER_PASS];
+} isal_hip_xrows;
+void isal_hip_xor_rows(int k, int rows, const unsigned char *gftbls, isal_hip_xrows *x);
+
 /* Launch counter shared by the shim and the launchers. */
 void isal_hip_count_launch(void);
 
@@ -90,6 +103,7 @@ enum {
         ISAL_HIP_KNOB_CRC64_FUSED_U,
         ISAL_HIP_KNOB_CRC64_FUSED_PAIR,
         ISAL_HIP_KNOB_CRC64_SRC_CHAIN, /* lds(0) | reg(1) */
+        ISAL_HIP_KNOB_CRC_XROWS,       /* 0: checksum 0/1 parity rows too (no derivation) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);
@@ -198,9 +212,9 @@ int isal_hip_launch_crc64(const uint64_t *d_ptrs, int ptr_stride, int nsh, long 
  * len >= ISAL_HIP_CRC_TILE and k <= ISAL_HIP_CRC64_MAX_FUSED_K. */
 #define ISAL_HIP_CRC64_MAX_FUSED_K 32 /* source chains: k * 2 KiB of LDS */
 int isal_hip_launch_encode_crc64(const uint64_t *d_ptrs, int k, int rows, long long nstripes,
-                                 int len, const uint32_t *d_tbl, int refl, int tt,
-                                 const uint64_t *d_tabs, uint64_t *d_part, uint64_t init_term,
-                                 uint64_t *out, void *stream);
+                                 int len, const uint32_t *d_tbl, const isal_hip_xrows *xr, int refl,
+                                 int tt, const uint64_t *d_tabs, uint64_t *d_part,
+                                 uint64_t init_term, uint64_t *out, void *stream);
 
 uint32_t isal_hip_crc32c_mulmod(uint32_t a, uint32_t b);
 uint32_t isal_hip_crc32c_xpow8n(unsigned long long n);
@@ -219,13 +233,17 @@ int isal_hip_launch_crc(const uint64_t *d_ptrs, int ptr_stride, int idx0, int ns
  * sources (shards 0..k-1) and the rows outputs (shards k..k+rows-1). Needs
  * 16-byte aligned shards, len % 16 == 0 and k <= ISAL_HIP_CRC_MAX_FUSED_K. */
 int isal_hip_launch_encode_crc(const uint64_t *d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
-                               const uint32_t *d_tbl, int len, int k, int rows, long long nstripes,
-                               int tt, const uint32_t *d_tabs, uint32_t *d_part, uint32_t *d_tail,
-                               void *stream);
-/* out[sh] = crc32_iscsi of shard sh (sh < nsh) from its partials. */
+                               const uint32_t *d_tbl, const isal_hip_xrows *xr, int len, int k,
+                               int rows, long long nstripes, int tt, const uint32_t *d_tabs,
+                               uint32_t *d_part, uint32_t *d_tail, void *stream);
+/* out[sh] = crc32_iscsi of shard sh (sh < nsh, nsh_stripe shards per stripe)
+ * from its partials. x0_src != 0: shard x0_shard of each stripe (row 0 of a
+ * fused encode under X0) is derived as the XOR of the partials of the source
+ * shards in the x0_src mask. */
 int isal_hip_launch_crc_combine(const uint32_t *d_part, const uint32_t *d_tail,
                                 const uint32_t *d_plan, long long nblk, int has_tail,
-                                unsigned int init, uint32_t *out, long long nsh, void *stream);
+                                unsigned int init, uint32_t *out, long long nsh, int nsh_stripe,
+                                int x0_shard, unsigned long long x0_src, void *stream);
 
 #ifdef __cplusplus
 }

@@ -774,6 +774,7 @@ struct isal_hip_batch {
         int len, k, rows, nstripes, device, vec16;
         uint64_t *d_ptrs;
         uint32_t *d_tbl;
+        isal_hip_xrows xr; /* 0/1 parity rows: CRCs derived, not computed */
         /* CRC32C state, allocated on first use: kernel tables + combine plan,
          * and the per-lane partials (crc_kernels.hip) */
         isal_hip_crc_geom crc;
@@ -849,6 +850,7 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         if (!h)
                 return ISAL_HIP_ENOMEM;
         isal_hip_build_tables(b->k, b->rows, gftbls, h);
+        isal_hip_xor_rows(b->k, b->rows, gftbls, &b->xr);
         if (!b->d_tbl) {
                 if (hipMalloc((void **) &b->d_tbl, n * 4 + 4) != hipSuccess) {
                         free(h);
@@ -964,13 +966,15 @@ batch_crc_setup(isal_hip_batch *b)
         return ISAL_HIP_OK;
 }
 
+/* x0: the fused kernel left parity row 0 to be derived (isal_hip_xrows) */
 static int
-batch_crc_finish(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+batch_crc_finish(isal_hip_batch *b, unsigned int init, unsigned int *crc, int x0, void *stream)
 {
         const long long nsh = (long long) b->nstripes * (b->k + b->rows);
         return isal_hip_launch_crc_combine(b->d_part, b->d_tail, b->d_crc + ISAL_HIP_CRC_TAB_DWORDS,
                                            b->crc.nblk, b->crc.tail != 0, init, (uint32_t *) crc,
-                                           nsh, stream)
+                                           nsh, b->k + b->rows, b->k,
+                                           x0 ? b->xr.src[0] : 0ull, stream)
                        ? ISAL_HIP_EHIP
                        : ISAL_HIP_OK;
 }
@@ -1000,7 +1004,7 @@ isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void
                                 b->vec16, b->crc.tt, b->d_crc, b->d_part, b->d_tail,
                                 b->k + b->rows, 0, stream))
                 return ISAL_HIP_EHIP;
-        return batch_crc_finish(b, init, crc, stream);
+        return batch_crc_finish(b, init, crc, 0, stream);
 }
 
 /* ---- CRC64 of the batch's shards (isal_hip.h) ----------------------------- */
@@ -1080,7 +1084,7 @@ isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long i
             b->k >= 1 && b->k <= ISAL_HIP_CRC64_MAX_FUSED_K)
                 /* one pass over the stripe: encode + CRC64 of all k + rows shards */
                 return isal_hip_launch_encode_crc64(
-                               b->d_ptrs, b->k, b->rows, b->nstripes, b->len, b->d_tbl,
+                               b->d_ptrs, b->k, b->rows, b->nstripes, b->len, b->d_tbl, &b->xr,
                                isal_hip_crc64_is_refl(variant), b->c64_tt, b->d_c64tab[variant],
                                b->d_c64part, isal_hip_crc64_init_term(variant, b->len, init),
                                (uint64_t *) crc, stream)
@@ -1095,7 +1099,7 @@ isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long i
 int
 isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
 {
-        int r;
+        int r, x0 = 0;
         if (!b || !crc)
                 return ISAL_HIP_EINVAL;
         if (b->len == 0)
@@ -1103,11 +1107,13 @@ isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *cr
         if ((r = batch_crc_setup(b)) != ISAL_HIP_OK)
                 return r;
         if (b->vec16 && b->len % 16 == 0 && b->k >= 1 && b->k <= ISAL_HIP_CRC_MAX_FUSED_K) {
-                /* one pass over the stripe: encode + CRC of all k + rows shards */
-                if (isal_hip_launch_encode_crc(b->d_ptrs, b->k + b->rows, 0, b->k, b->d_tbl, b->len,
-                                               b->k, b->rows, b->nstripes, b->crc.tt, b->d_crc,
-                                               b->d_part, b->d_tail, stream))
+                /* one pass over the stripe: encode + CRC of all k + rows shards
+                 * (row 0 derived from the sources when it is a 0/1 row) */
+                if (isal_hip_launch_encode_crc(b->d_ptrs, b->k + b->rows, 0, b->k, b->d_tbl, &b->xr,
+                                               b->len, b->k, b->rows, b->nstripes, b->crc.tt,
+                                               b->d_crc, b->d_part, b->d_tail, stream))
                         return ISAL_HIP_EHIP;
+                x0 = b->xr.rows & 1u;
         } else {
                 /* unaligned shards, ragged len or very wide k: encode, then CRC */
                 if (isal_hip_batch_encode(b, stream) != ISAL_HIP_OK)
@@ -1117,5 +1123,5 @@ isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *cr
                                         b->d_tail, b->k + b->rows, 0, stream))
                         return ISAL_HIP_EHIP;
         }
-        return batch_crc_finish(b, init, crc, stream);
+        return batch_crc_finish(b, init, crc, x0, stream);
 }

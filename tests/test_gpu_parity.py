@@ -600,6 +600,51 @@ def test_encode_crc_tiles_per_workgroup(engine, oracle, gpu, monkeypatch, k, row
     b.close()
 
 
+@pytest.mark.parametrize("xrows", ["1", "0"])
+@pytest.mark.parametrize("k,n,tt", [(10, 4096 * 37 + 2048, 4), (7, 65536, None), (10, 65536, None)])
+def test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, xrows, k, n, tt):
+    """Parity rows whose coefficients are all 0/1 (all-ones, RAID-P-like rows
+    with zeros, an all-zero row) get their CRC32C / CRC64 from the sources'
+    partials instead of being checksummed (ISAL_HIP_CRC_XROWS=1, default);
+    both ways every CRC == the oracle, full and ragged tiles, register and
+    LDS source chains."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_CRC_XROWS", xrows)
+    if tt:
+        _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
+    rows, ns = 5, 3
+    coef = np.concatenate([np.ones(k, np.uint8),                              # all ones
+                           (np.arange(k) % 2).astype(np.uint8),               # 0/1 mix
+                           fill_bytes(k, 5),                                  # general
+                           np.zeros(k, np.uint8),                             # all zero
+                           (np.arange(k) % 3 == 0).astype(np.uint8)])         # sparse 0/1
+    tbls = engine.ec_init_tables(k, rows, coef)
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 31 + k)
+    h = _host(data)
+    want = _oracle_encode_all(oracle, coef, k, rows, [[h[s, j] for j in range(k)] for s in range(ns)])
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    c32 = torch.zeros(ns * (k + rows), dtype=torch.int32, device=gpu)
+    b.encode_crc(0x1234567, c32, 0)
+    torch.cuda.synchronize()
+    hc = _host(coding)
+    g32 = [int(v) & 0xFFFFFFFF for v in c32.tolist()]
+    coding.zero_()
+    c64 = torch.zeros(ns * (k + rows), dtype=torch.int64, device=gpu)
+    b.encode_crc64(6, 0xABCDEF, c64, 0)
+    torch.cuda.synchronize()
+    g64 = [int(v) & 0xFFFFFFFFFFFFFFFF for v in c64.tolist()]
+    assert np.array_equal(_host(coding), hc)
+    for s in range(ns):
+        shards = [h[s, j] for j in range(k)] + want[s]
+        for l in range(rows):
+            assert np.array_equal(hc[s, l], want[s][l]), (s, l)
+        for i, buf in enumerate(shards):
+            assert g32[s * (k + rows) + i] == oracle.crc32_iscsi(buf, 0x1234567), (s, i, "crc32c")
+            assert g64[s * (k + rows) + i] == oracle.crc64(6, buf, 0xABCDEF), (s, i, "crc64")
+    b.close()
+
+
 def test_encode_crc_c2_full_size(engine, oracle, gpu):
     """C2 at full size through the fused path: parity identical to the plain
     encode kernel's, CRCs == oracle on sampled stripes and == the standalone

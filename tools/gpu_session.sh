@@ -147,6 +147,11 @@ for s in $STEPS; do
                 run route_crossover 300 python tools/route_crossover.py
                 run latency_probe 120 python tools/latency_probe.py
                 ;;
+        crcbench)
+                for wl in encode-crc encode-crc64 crc crc64; do
+                        run bench_$wl 300 python bench.py --workload $wl --no-cpu-baseline
+                done
+                ;;
         e2etrace)
                 for dp in 2 6; do
                         run e2etrace_d$dp 300 rocprofv3 --memory-copy-trace --kernel-trace --stats --output-format csv -d "$OUT/e2etrace_d$dp" -o t -- python3 bench.py --workload e2e-encode --steps 100 --warmup 10 --depth $dp
