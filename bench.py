@@ -71,6 +71,9 @@ def parse_args(argv=None):
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N>1 control-plane backend (nccl = RCCL over xGMI; gloo lets several "
                          "ranks share one GPU for testing)")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="initialise the process group even at world size 1 (exercises the RCCL "
+                         "control plane on a one-GPU box)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the distributed harness without a GPU (gloo, dummy step)")
     return ap.parse_args(argv)
@@ -81,7 +84,7 @@ def parse_args(argv=None):
 # ---------------------------------------------------------------------------
 
 class Dist:
-    def __init__(self, dry: bool, backend: str = "nccl"):
+    def __init__(self, dry: bool, backend: str = "nccl", always: bool = False):
         self.rank = int(os.environ.get("RANK", 0))
         self.world = int(os.environ.get("WORLD_SIZE", 1))
         self.local_rank = int(os.environ.get("LOCAL_RANK", 0))
@@ -93,8 +96,13 @@ class Dist:
 
             # one process per GPU; ranks beyond the device count (gloo tests) share
             self.gpu = self.local_rank % max(1, torch.cuda.device_count())
-        if self.world > 1:
+        if self.world > 1 or always:
             import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", str(self.rank))
+            os.environ.setdefault("WORLD_SIZE", str(self.world))
 
             self.backend = "gloo" if dry else backend  # nccl == RCCL on ROCm
             if self.backend == "gloo":
@@ -566,7 +574,7 @@ def total_stripes_run(args, d: Dist, a, k, p, n):
 
 def main(argv=None):
     args = parse_args(argv)
-    d = Dist(args.dry_run, args.dist_backend)
+    d = Dist(args.dry_run, args.dist_backend, args.dist_always)
     if args.dry_run:
         return dry_run(args, d)
 
@@ -749,6 +757,15 @@ def main(argv=None):
         for i, e in enumerate(errs):
             ok &= bool(torch.equal(out[:, i], data[:, e]))
     self_check = None if args.workload == "update" else bool(d.max(0.0 if ok else 1.0) == 0.0)
+    digest = None
+    if args.workload in ("encode", "decode"):
+        # control-plane digest of every rank's shards: CRC32C of all sources and
+        # parity of the batch, summed on each rank and all-reduced (RCCL)
+        dg = torch.zeros(S * (batch.k + batch.rows), dtype=torch.int32, device=dev)
+        batch.crc(0xFFFFFFFF, dg, h)
+        torch.cuda.synchronize(dev)
+        digest = d.sum_i64([int((dg.to(torch.int64) & 0xFFFFFFFF).sum().item())])[0]
+        del dg
 
     if args.workload == "update":
         step_bytes = (1 + 2 * p) * n * S
@@ -776,10 +793,12 @@ def main(argv=None):
         "config": {
             "workload": workload,
             "k": k, "p": p, "shard_bytes": n, "stripes_per_gpu": S,
+            "stripe_ranges": [[r * S, (r + 1) * S] for r in range(d.world)],
             "parallelism": f"stripes sharded over {d.world} GPU(s), no data-path collective",
         },
         "payload_gib_s": round(k * n * S * args.steps * d.world / wall / GIB, 2),
         "self_check": self_check,
+        "shard_crc32c_digest": digest,
         "roofline": {
             "bound": "hbm",
             "kernel": kernel,

@@ -19,6 +19,7 @@
 extern "C" void gf_gen_rs_matrix(unsigned char* a, int m, int k);
 extern "C" void ec_init_tables(int k, int rows, unsigned char* a, unsigned char* gftbls);
 extern "C" void isal_hip_count_launch(void) {}
+extern "C" long long isal_hip_knob(int) { return -1; }
 
 #define CK(x)                                                                          \
   do {                                                                                 \
@@ -233,6 +234,11 @@ int main(int argc, char** argv) {
                                     st, d_ptrs, stride, len, nitems, tiles, (uint32_t*)sinkp);  \
                }});
   PATTERNB(2, 2, "buf r10w4 nt/nt")
+  // the decode (C3) mix: 10 survivors read, 3 recovered shards written
+  V.push_back({"buf r10w3 nt/nt (decode mix)", 13.0 * shard * S, [=](hipStream_t st) {
+                 hipLaunchKernelGGL((mem_pattern_buf<10, 3, 2, 2>), dim3(nitems), dim3(256), 0, st,
+                                    d_ptrs, stride, len, nitems, tiles, (uint32_t*)sinkp);
+               }});
   PATTERNB(0x12, 0x12, "buf r10w4 sc1nt/sc1nt")
   PATTERNB(0x13, 0x13, "buf r10w4 sc0sc1nt/sc0sc1nt")
   PATTERNB(0x10, 0x10, "buf r10w4 sc1/sc1")

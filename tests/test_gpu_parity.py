@@ -1164,6 +1164,32 @@ def test_bench_two_ranks_on_one_gpu(gpu):
     assert out["scaling"] == "strong" and out["value"] > 0
 
 
+def test_bench_rccl_control_plane_single_rank(gpu):
+    """The nccl (= RCCL) branch of bench.py's Dist on this one-GPU box: a
+    world-size-1 process group over RCCL carries the matrix broadcast, the
+    barriers, the max of the timings and the sums of counts / digests / ranges,
+    in both the C2 (weak) and the C5 (--total-stripes) modes."""
+    import json
+    import socket
+    import sys
+
+    for extra in ([], ["--total-stripes", "100"]):
+        sock = socket.socket()
+        sock.bind(("127.0.0.1", 0))
+        port = sock.getsockname()[1]
+        sock.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", str(port),
+               os.path.join(ecutil.REPO, "bench.py"), "--dist-always", "--dist-backend", "nccl",
+               "--stripes", "32", "--len", "65536", "--steps", "3", "--warmup", "1",
+               "--no-cpu-baseline"] + extra
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ecutil.REPO)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        assert out["n_gpus"] == 1 and out["self_check"] is True and out["value"] > 0, out
+        assert out["shard_crc32c_digest"] > 0
+
+
 def test_multi_device_encode_host_stripes_vs_oracle(engine, oracle, gpu):
     """isal_hip_multi_*: host stripes over every visible GPU (here: one), each
     GPU its contiguous range through its own pipeline; == oracle."""
