@@ -104,6 +104,7 @@ enum {
         ISAL_HIP_KNOB_CRC64_FUSED_PAIR,
         ISAL_HIP_KNOB_CRC64_SRC_CHAIN, /* lds(0) | reg(1) */
         ISAL_HIP_KNOB_CRC_XROWS,       /* 0: checksum 0/1 parity rows too (no derivation) */
+        ISAL_HIP_KNOB_FAULT,           /* fault-injection site of GPU-routed calls (tests) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

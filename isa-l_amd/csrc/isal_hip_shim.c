@@ -406,6 +406,34 @@ typedef struct {
         unsigned long long first_bad;
 } gpu_res;
 
+/* Fault injection (tests): ISAL_HIP_FAULT=<site> makes every GPU-routed call
+ * fail at that site as if the HIP call there had returned an error, without
+ * issuing it — the fallback paths then run for real. Sites: */
+enum {
+        FAULT_NONE = 0,
+        FAULT_ALLOC = 1,  /* staging / argument buffer allocation */
+        FAULT_H2D = 2,    /* a host-to-device copy */
+        FAULT_LAUNCH = 3, /* the kernel launch */
+        FAULT_D2H = 4,    /* the device-to-host copy of output row 1 (chunked) or of the outputs */
+        FAULT_SYNC = 5,   /* the final stream synchronisation */
+};
+
+static int
+fault_at(int site)
+{
+        return site != FAULT_NONE && isal_hip_knob(ISAL_HIP_KNOB_FAULT) == site;
+}
+
+#define GPU_TRY_AT(r, site, call)                                                                  \
+        do {                                                                                       \
+                hipError_t e_ = fault_at(site) ? hipErrorOutOfMemory : (call);                     \
+                if (e_ != hipSuccess) {                                                            \
+                        (r).err = e_;                                                              \
+                        (r).what = #call;                                                          \
+                        return (r);                                                                \
+                }                                                                                  \
+        } while (0)
+
 #define GPU_TRY(r, call)                                                                           \
         do {                                                                                       \
                 hipError_t e_ = (call);                                                            \
@@ -430,7 +458,7 @@ gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
         size_t upload;
         uint64_t *h_ptrs;
 
-        GPU_TRY(r, ensure_args(c, L.total));
+        GPU_TRY_AT(r, FAULT_ALLOC, ensure_args(c, L.total));
         h = (char *) c->h_args;
         dv = zero_copy ? (char *) c->h_args_dev : (char *) c->d_args; /* what kernels see */
         h_ptrs = (uint64_t *) h;
@@ -456,21 +484,21 @@ gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
                         vec16 = 0;
         }
         if (!zero_copy)
-                GPU_TRY(r, hipMemcpyAsync(c->d_args, h, upload, hipMemcpyHostToDevice, c->stream));
-        GPU_TRY(r, launch_op(c, op, dv, &L, nptr, nsrc, len, 0, k, rows, vec_i, vec16, &nslots));
+                GPU_TRY_AT(r, FAULT_H2D, hipMemcpyAsync(c->d_args, h, upload, hipMemcpyHostToDevice, c->stream));
+        GPU_TRY_AT(r, FAULT_LAUNCH, launch_op(c, op, dv, &L, nptr, nsrc, len, 0, k, rows, vec_i, vec16, &nslots));
         if (!zero_copy) {
                 if (op == OP_VERIFY)
                         GPU_TRY(r, hipMemcpyAsync(h + L.slots_off, (char *) c->d_args + L.slots_off,
                                                   (size_t) nslots * 8, hipMemcpyDeviceToHost,
                                                   c->stream));
                 else if (first_out >= 0)
-                        GPU_TRY(r, hipMemcpyAsync(h + L.stage_off + (size_t) first_out * L.slot,
+                        GPU_TRY_AT(r, FAULT_D2H, hipMemcpyAsync(h + L.stage_off + (size_t) first_out * L.slot,
                                                   (char *) c->d_args + L.stage_off +
                                                           (size_t) first_out * L.slot,
                                                   (size_t) (nstage - first_out) * L.slot,
                                                   hipMemcpyDeviceToHost, c->stream));
         }
-        GPU_TRY(r, hipStreamSynchronize(c->stream));
+        GPU_TRY_AT(r, FAULT_SYNC, hipStreamSynchronize(c->stream));
         if (op == OP_VERIFY) {
                 r.first_bad = min_slot((const unsigned long long *) (h + L.slots_off), nslots);
         } else {
@@ -505,7 +533,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                         per = 4096;
                 chunk = (size_t) len < per ? (size_t) len : per;
                 slot = (chunk + 255) & ~(size_t) 255; /* keep every slot 256-B aligned */
-                GPU_TRY(r, ensure_stage(c, slot * (size_t) nstage));
+                GPU_TRY_AT(r, FAULT_ALLOC, ensure_stage(c, slot * (size_t) nstage));
         } else {
                 chunk = (size_t) len;
                 slot = 0;
@@ -530,7 +558,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                                 /* sources, and outputs of a read-modify-write update or
                                  * of a verify, go in */
                                 if (i < nsrc || op != OP_ENCODE)
-                                        GPU_TRY(r, hipMemcpyAsync(st, host + c0, (size_t) clen,
+                                        GPU_TRY_AT(r, FAULT_H2D, hipMemcpyAsync(st, host + c0, (size_t) clen,
                                                                   hipMemcpyHostToDevice, c->stream));
                         }
                         h_ptrs[i] = d;
@@ -539,7 +567,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                 }
                 GPU_TRY(r, hipMemcpyAsync(c->d_args, c->h_args, L.args_bytes,
                                           hipMemcpyHostToDevice, c->stream));
-                GPU_TRY(r, launch_op(c, op, (char *) c->d_args, &L, nptr, nsrc, clen, c0, k, rows,
+                GPU_TRY_AT(r, FAULT_LAUNCH, launch_op(c, op, (char *) c->d_args, &L, nptr, nsrc, clen, c0, k, rows,
                                      vec_i, vec16, &nslots));
                 if (op == OP_VERIFY) {
                         GPU_TRY(r, hipMemcpyAsync((char *) c->h_args + L.slots_off,
@@ -562,7 +590,8 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                         if (flag[i])
                                 continue;
                         if (i >= nsrc) {
-                                GPU_TRY(r, hipMemcpyAsync(dst[i - nsrc] + c0,
+                                GPU_TRY_AT(r, i - nsrc == 1 ? FAULT_D2H : FAULT_NONE,
+                                           hipMemcpyAsync(dst[i - nsrc] + c0,
                                                           c->d_stage + (size_t) s * slot,
                                                           (size_t) clen, hipMemcpyDeviceToHost,
                                                           c->stream));
@@ -570,7 +599,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                         }
                         s++;
                 }
-                GPU_TRY(r, hipStreamSynchronize(c->stream));
+                GPU_TRY_AT(r, FAULT_SYNC, hipStreamSynchronize(c->stream));
                 r.done = c0 + clen;
                 r.rows_out = 0;
         }

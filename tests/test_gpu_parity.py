@@ -354,6 +354,36 @@ def test_config_c2_c3_full_size(engine, oracle, gpu):
     dec.close()
 
 
+@pytest.mark.parametrize("site", [1, 2, 3, 4, 5])
+def test_hip_failure_falls_back_to_cpu_route(engine, oracle, gpu, monkeypatch, site):
+    """SURVEY §5 'never fail where the reference succeeds': ISAL_HIP_FAULT makes
+    every GPU-routed host call fail at one site (allocation, H2D, launch, D2H
+    of output row 1, final sync). The call must still return the oracle's
+    bytes — from the CPU route, for the columns not yet final — and count a
+    fallback; an update that failed after some parity rows were copied back
+    must not fold them twice. Zero-copy, packed and column-chunked calls."""
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", "auto")
+    _setenv(monkeypatch, "ISAL_HIP_CPU_MAX_BYTES", "0")  # host calls go to the GPU first
+    _setenv(monkeypatch, "ISAL_HIP_STAGE_MB", "1")       # several column chunks
+    _setenv(monkeypatch, "ISAL_HIP_FAULT", str(site))
+    rng = np.random.default_rng(site)
+    for n in (4096, 65536 + 48, 300000):                 # zero-copy, packed, chunked
+        k, rows = 6, 5
+        coef = fill_bytes(k * rows, n + site)
+        tbls = engine.ec_init_tables(k, rows, coef)
+        src = [fill_bytes(n, 17 * site + j) for j in range(k)]
+        want = oracle.encode(coef, k, rows, src)
+        before = engine.fallbacks()
+        got = [np.zeros(n, np.uint8) for _ in range(rows)]
+        engine.ec_encode_data(n, k, rows, tbls, src, got)
+        assert all(np.array_equal(a, b) for a, b in zip(got, want)), ("encode", site, n)
+        upd = [np.zeros(n, np.uint8) for _ in range(rows)]
+        for v in rng.permutation(k):
+            engine.ec_encode_data_update(n, k, rows, int(v), tbls, src[int(v)], upd)
+        assert all(np.array_equal(a, b) for a, b in zip(upd, want)), ("update", site, n)
+        assert engine.fallbacks() > before, (site, n)
+
+
 def test_dropin_call_ordered_after_default_stream_work(engine, oracle, gpu):
     """A synchronous drop-in call on device shards sees work the caller queued
     on the legacy default stream just before it (torch writes the sources and
