@@ -643,8 +643,9 @@ def main(argv=None):
             bytes_per_launch = (k + p) * n * S
             if args.workload == "encode-crc":
                 u = enc_group(k)  # one load group (k == U): source CRC chains in registers
-                reg = k == u and os.environ.get("ISAL_HIP_CRC_SRC_CHAIN", "reg") != "lds"
-                kernel = f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true, true>"
+                reg = k == u and os.environ.get("ISAL_HIP_CRC_SRC_CHAIN") == "reg"
+                x0 = "false" if reg else "true"  # Vandermonde row 0 derived (LDS-chain variant)
+                kernel = f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true, {x0}>"
                 workload = (f"C2 encode + CRC32C (crc32_iscsi) of all k+p shards in one pass: k={k} "
                             f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
             else:

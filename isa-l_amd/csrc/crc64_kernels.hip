@@ -240,15 +240,11 @@ __device__ __forceinline__ uint64_t lane_tree(uint64_t* red, const uint64_t* tre
 //      the tree, so lane q-1's chunk is the last one;
 //  s = Z^(16q)(X) ^ T, then the last tail % 16 bytes one at a time;
 //  crc64 = ~(Z^len(~init) ^ s).
-// x0_src != 0: shard x0_shard of every stripe (parity row 0 of a fused X0
-// encode) has no partials of its own; they are the XOR of the partials of the
-// sources in x0_src. (Its ragged tail is read from the shard like any other.)
 template <bool REFL>
 __global__ __launch_bounds__(kBlock) void crc64_combine(
     const uint64_t* __restrict__ part, const uint64_t* __restrict__ ptrs, int ptr_stride, int nsh,
     int len, unsigned nblk, unsigned nfull, const uint64_t* __restrict__ tabs, uint64_t init_term,
-    uint64_t* __restrict__ out, unsigned nshard_total, unsigned x0_shard,
-    unsigned long long x0_src) {
+    uint64_t* __restrict__ out, unsigned nshard_total) {
   __shared__ uint64_t lt[ISAL_HIP_CRC64_COMBINE_ENTRIES];
   __shared__ uint64_t red[kBlock];
   load_lds<ISAL_HIP_CRC64_COMBINE_ENTRIES>(lt, tabs);
@@ -261,19 +257,10 @@ __global__ __launch_bounds__(kBlock) void crc64_combine(
     uint64_t x = 0, tq = 0;
     if (nblk) {
       const uint64_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + threadIdx.x;
-      const uint64_t* ps = part + static_cast<size_t>(stripe) * nsh * nblk * kBlock + threadIdx.x;
-      const bool derived = x0_src && i == x0_shard;
       uint64_t h = 0;
-      for (unsigned b = 0; b < nblk; ++b) {
-        uint64_t v = 0;
-        if (!derived) {
-          v = pp[static_cast<size_t>(b) * kBlock];
-        } else {
-          for (unsigned j = 0; j < x0_shard; ++j)
-            if ((x0_src >> j) & 1ull) v ^= ps[(static_cast<size_t>(j) * nblk + b) * kBlock];
-        }
-        h = apply_op(lt + (b + 1 == nblk ? ISAL_HIP_CRC64_OP_LAST : ISAL_HIP_CRC64_OP_BLOCK), h) ^ v;
-      }
+      for (unsigned b = 0; b < nblk; ++b)
+        h = apply_op(lt + (b + 1 == nblk ? ISAL_HIP_CRC64_OP_LAST : ISAL_HIP_CRC64_OP_BLOCK), h) ^
+            pp[static_cast<size_t>(b) * kBlock];
       red[threadIdx.x] = h;
       __syncthreads();
       x = lane_tree(red, lt + ISAL_HIP_CRC64_OP_TREE);
@@ -382,15 +369,15 @@ constexpr int fused64_waves() {
 }
 
 // X0: parity row 0 has only 0/1 coefficients (RS Vandermonde row 0, RAID P):
-// it is the XOR of some sources, so its chain is not computed and
-// crc64_combine derives its partials from those sources' (CRC is
-// GF(2)-linear). A compile-time variant: a runtime row mask in the tile loop
-// costs registers.
+// it is the XOR of the sources in x0src, so (CRC being GF(2)-linear) its
+// chain is not computed per tile but formed once per block from those
+// sources' chains. A compile-time variant: a runtime row mask in the tile
+// loop costs registers.
 template <int P, int U, bool REG, bool X0 = false>
 __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encode_crc64_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, const uint32_t* __restrict__ tbl, int len,
     int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged, int pair,
-    const uint64_t* __restrict__ tabs, uint64_t* __restrict__ part) {
+    unsigned long long x0src, const uint64_t* __restrict__ tabs, uint64_t* __restrict__ part) {
   __shared__ uint64_t lt[kKernTab + kCE + kOp];
   extern __shared__ uint64_t la[];  // [k][kBlock] source chains when !REG
   load_lds<kKernTab>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
@@ -503,6 +490,18 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
           store16<kNT>(sp[k + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
       }
     }
+    if constexpr (X0) {  // row 0 = XOR of the sources in x0src: so is its chain
+      uint64_t v = 0;
+      if constexpr (REG) {
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+          if ((x0src >> j) & 1ull) v ^= ra[j];
+      } else {
+        for (int j = 0; j < k; ++j)
+          if ((x0src >> j) & 1ull) v ^= la[j * kBlock + threadIdx.x];
+      }
+      ao[0] = v;
+    }
     uint64_t* pp = part + (static_cast<size_t>(stripe) * nsh * nblk + blk) * kBlock + threadIdx.x;
     const size_t sstep = static_cast<size_t>(nblk) * kBlock;
     if constexpr (REG) {
@@ -512,7 +511,7 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
       for (int j = 0; j < k; ++j) pp[j * sstep] = la[j * kBlock + threadIdx.x];
     }
 #pragma unroll
-    for (int l = X0 ? 1 : 0; l < P; ++l) pp[(k + l) * sstep] = ao[l];
+    for (int l = 0; l < P; ++l) pp[(k + l) * sstep] = ao[l];
   }
 }
 
@@ -553,7 +552,7 @@ void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_
   hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, REG, X0>), dim3(grid), dim3(kBlock), LDS, s, ptrs, \
                      ptr_stride, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),             \
                      static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), ragged,         \
-                     pair_step(), tabs, part)
+                     pair_step(), xr.src[0], tabs, part)
   const size_t lds = static_cast<size_t>(k) * kBlock * 8;
   if (k == U && src_chain_reg64()) {
     if (xr.rows & 1u) FUSED64_LAUNCH(true, true, 0); else FUSED64_LAUNCH(true, false, 0);
@@ -579,18 +578,17 @@ void fused64_pass(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_st
 
 int launch_combine64(const uint64_t* part, const uint64_t* ptrs, int ptr_stride, int nsh, int len,
                      const isal_hip_crc64_geom& g, int refl, const uint64_t* tabs,
-                     uint64_t init_term, uint64_t* out, unsigned nshard, hipStream_t s,
-                     unsigned x0_shard = 0, unsigned long long x0_src = 0) {
+                     uint64_t init_term, uint64_t* out, unsigned nshard, hipStream_t s) {
   // each combine workgroup copies the 52 KB table set once: cap the grid
   const unsigned grid = nshard < 2048 ? nshard : 2048;
   if (refl)
     hipLaunchKernelGGL(crc64_combine<true>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
                        nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
-                       tabs, init_term, out, nshard, x0_shard, x0_src);
+                       tabs, init_term, out, nshard);
   else
     hipLaunchKernelGGL(crc64_combine<false>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
                        nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
-                       tabs, init_term, out, nshard, x0_shard, x0_src);
+                       tabs, init_term, out, nshard);
   isal_hip_count_launch();
   return static_cast<int>(hipGetLastError());
 }
@@ -672,8 +670,7 @@ extern "C" int isal_hip_launch_encode_crc64(const uint64_t* d_ptrs, int k, int r
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);
     const int r = launch_combine64(part, ptrs, nsh, nsh, len, g, refl, d_tabs, init_term,
-                                   out + s0 * nsh, static_cast<unsigned>(ns * nsh), s,
-                                   static_cast<unsigned>(k), (xr.rows & 1u) ? xr.src[0] : 0ull);
+                                   out + s0 * nsh, static_cast<unsigned>(ns * nsh), s);
     if (r) return r;
   }
   return 0;

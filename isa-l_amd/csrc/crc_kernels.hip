@@ -328,18 +328,18 @@ constexpr int crc_waves() {
 
 // SRC: this pass also checksums the k sources (the first pass of a stripe).
 // X0 (SRC passes only): parity row 0 has only 0/1 coefficients (RS Vandermonde
-// row 0, RAID P), so it is the XOR of some sources and — CRC being
-// GF(2)-linear in the data — crc32c_combine derives its checksum from those
-// sources' partials; the kernel neither chains nor stores it. (A compile-time
-// choice: a runtime row mask inside the tile loop costs the register-tight
-// kernel its registers.)
+// row 0, RAID P), so it is the XOR of the sources in x0src and — CRC being
+// GF(2)-linear in the data — so is its chain: it is formed once per block
+// from those sources' chains instead of per tile. (A compile-time choice: a
+// runtime row mask inside the tile loop costs the register-tight kernel its
+// registers.)
 template <int P, class Pol, bool REG, bool SRC, bool X0 = false>
 __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_encode_crc_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned nblk, unsigned tt,
-    unsigned nfull, unsigned ntiles, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part,
-    uint32_t* __restrict__ tail, int nshard_total, int out_shard0) {
-  static_assert(!X0 || SRC, "row 0 is derived from this pass's source partials");
+    unsigned nfull, unsigned ntiles, unsigned long long x0src, const uint32_t* __restrict__ tabs,
+    uint32_t* __restrict__ part, uint32_t* __restrict__ tail, int nshard_total, int out_shard0) {
+  static_assert(!X0 || SRC, "row 0 is derived from this pass's source chains");
   constexpr int kFull = SRC ? (REG ? kFeedReg : kFeedLds) : kFeedNone;
   constexpr int kRag = SRC ? kFeedTail : kFeedNone;
   constexpr int NR = REG ? Pol::U : 1;
@@ -416,8 +416,13 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
         for (int l = 0; l < P; ++l) {
           store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
                            len);
-          if (X0 && l == 0) continue;  // derived by crc32c_combine
-          const uint32_t c = chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+          uint32_t c = 0;
+          if (X0 && l == 0) {  // the sources' tail chunks: this lane wrote them above
+            for (int j = 0; j < k; ++j)
+              if ((x0src >> j) & 1ull) c ^= trow[j * kBlock + threadIdx.x];
+          } else {
+            c = chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+          }
           trow[(out_shard0 + l) * kBlock + threadIdx.x] = c;
         }
       } else {  // lane past len
@@ -427,8 +432,20 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
         for (int l = 0; l < P; ++l) trow[(out_shard0 + l) * kBlock + threadIdx.x] = 0;
       }
     }
+    if constexpr (X0) {  // row 0's chain = XOR of its sources' chains
+      uint32_t v = 0;
+      if constexpr (REG) {
 #pragma unroll
-    for (int l = X0 ? 1 : 0; l < P; ++l)
+        for (int j = 0; j < NR; ++j)
+          if ((x0src >> j) & 1ull) v ^= ra[j];
+      } else {
+        for (int j = 0; j < k; ++j)
+          if ((x0src >> j) & 1ull) v ^= la[j * kBlock + threadIdx.x];
+      }
+      ao[0] = v;
+    }
+#pragma unroll
+    for (int l = 0; l < P; ++l)
       part[((shard_s + out_shard0 + l) * nblk + blk) * kBlock + threadIdx.x] = ao[l];
     if constexpr (SRC) {
       if constexpr (REG) {
@@ -452,8 +469,7 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
 __global__ __launch_bounds__(kBlock) void crc32c_combine(
     const uint32_t* __restrict__ part, const uint32_t* __restrict__ tail,
     const uint32_t* __restrict__ plan, unsigned nblk, int has_tail, unsigned init,
-    uint32_t* __restrict__ out, unsigned nsh, unsigned nsh_stripe, unsigned x0_shard,
-    unsigned long long x0_src) {
+    uint32_t* __restrict__ out, unsigned nsh) {
   __shared__ uint32_t kt[2048];
   __shared__ uint32_t red[kBlock / 64];
   for (int i = threadIdx.x; i < 2048; i += kBlock) kt[i] = plan[i];
@@ -462,36 +478,15 @@ __global__ __launch_bounds__(kBlock) void crc32c_combine(
   const uint32_t cl = plan[2304 + threadIdx.x];
   const uint32_t xlen = plan[2560];
   for (unsigned sh = blockIdx.x; sh < nsh; sh += gridDim.x) {
-    // x0_src != 0: shard x0_shard of every stripe (parity row 0 of a fused
-    // encode with 0/1 coefficients) was not checksummed; its partials are the
-    // XOR of the partials of the sources in x0_src (CRC is GF(2)-linear)
-    const unsigned stripe = sh / nsh_stripe, i = sh - stripe * nsh_stripe;
-    const bool derived = x0_src && i == x0_shard;
-    const size_t s0 = static_cast<size_t>(stripe) * nsh_stripe;
-    auto partial = [&](unsigned b) {
-      if (!derived) return part[(static_cast<size_t>(sh) * nblk + b) * kBlock + threadIdx.x];
-      uint32_t v = 0;
-      for (unsigned j = 0; j < x0_shard; ++j)
-        if ((x0_src >> j) & 1ull) v ^= part[((s0 + j) * nblk + b) * kBlock + threadIdx.x];
-      return v;
-    };
+    const uint32_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + threadIdx.x;
     uint32_t h = 0;
     for (unsigned b = 0; b < nblk; ++b) {
       const uint32_t* k4 = (b + 1 == nblk) ? kt + 1024 : kt;
       h = xor3(k4[h & 0xff], k4[256 + ((h >> 8) & 0xff)], k4[512 + ((h >> 16) & 0xff)]) ^
-          k4[768 + (h >> 24)] ^ partial(b);
+          k4[768 + (h >> 24)] ^ pp[static_cast<size_t>(b) * kBlock];
     }
     uint32_t v = crc_mulmod(h, wl);
-    if (has_tail) {
-      uint32_t tl = 0;
-      if (!derived) {
-        tl = tail[static_cast<size_t>(sh) * kBlock + threadIdx.x];
-      } else {
-        for (unsigned j = 0; j < x0_shard; ++j)
-          if ((x0_src >> j) & 1ull) tl ^= tail[(s0 + j) * kBlock + threadIdx.x];
-      }
-      v ^= crc_mulmod(tl, cl);
-    }
+    if (has_tail) v ^= crc_mulmod(tail[static_cast<size_t>(sh) * kBlock + threadIdx.x], cl);
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -527,10 +522,13 @@ int enc_group_crc(int k) {
   return 4;
 }
 
-// ISAL_HIP_CRC_SRC_CHAIN=lds keeps the source chains in LDS even when the k
-// sources form one load group (tuning knob; default: registers).
+// Source chains in registers when the k sources form one load group only with
+// ISAL_HIP_CRC_SRC_CHAIN=reg: the register variant needs 153 VGPRs (3 waves
+// per SIMD) and was 2 % behind LDS chains on the C2 shape already in round 1
+// (profiles/r01_crc_tile_sweep.txt); LDS chains (117 VGPRs, 4 waves) also
+// take the X0 variant.
 bool src_chain_reg() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC_SRC_CHAIN) != 0;  // not "lds"
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC_SRC_CHAIN) == 1;  // "reg"
 }
 
 template <int P, int U>
@@ -542,16 +540,17 @@ void launch_fused(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs
   hipLaunchKernelGGL((ec_encode_crc_v16<P, FusedPol<U>, REG, SRC, X0>), dim3(grid), dim3(kBlock),  \
                      LDS, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems,                    \
                      static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),                   \
-                     static_cast<unsigned>(g.nfull), static_cast<unsigned>(g.ntiles), tabs, part, \
-                     tail, nshard_total, out_shard0)
+                     static_cast<unsigned>(g.nfull), static_cast<unsigned>(g.ntiles), xr.src[0],  \
+                     tabs, part, tail, nshard_total, out_shard0)
   const bool x0 = crc_src && (xr.rows & 1u);
   if (!crc_src)
     FUSED_LAUNCH(false, false, false, 0);
-  else if (k == U && src_chain_reg()) {  // one load group: source chains in registers
-    if (x0) FUSED_LAUNCH(true, true, true, 0); else FUSED_LAUNCH(true, true, false, 0);
-  } else {
-    if (x0) FUSED_LAUNCH(false, true, true, lds); else FUSED_LAUNCH(false, true, false, lds);
-  }
+  else if (k == U && src_chain_reg())  // one load group: source chains in registers (no X0:
+    FUSED_LAUNCH(true, true, false, 0);  // its 2 extra SGPRs make the register variant spill)
+  else if (x0)
+    FUSED_LAUNCH(false, true, true, lds);
+  else
+    FUSED_LAUNCH(false, true, false, lds);
 #undef FUSED_LAUNCH
 }
 
@@ -659,16 +658,12 @@ extern "C" int isal_hip_launch_encode_crc(const uint64_t* d_ptrs, int ptr_stride
 extern "C" int isal_hip_launch_crc_combine(const uint32_t* d_part, const uint32_t* d_tail,
                                            const uint32_t* d_plan, long long nblk, int has_tail,
                                            unsigned int init, uint32_t* out, long long nsh,
-                                           int nsh_stripe, int x0_shard,
-                                           unsigned long long x0_src, void* stream) {
+                                           void* stream) {
   if (nsh <= 0) return 0;
-  if (nsh_stripe <= 0 || (x0_src && (x0_shard < 0 || x0_shard > 64)))
-    return static_cast<int>(hipErrorInvalidValue);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned grid = nsh < 4096 ? static_cast<unsigned>(nsh) : 4096u;
   hipLaunchKernelGGL(crc32c_combine, dim3(grid), dim3(kBlock), 0, s, d_part, d_tail, d_plan,
-                     static_cast<unsigned>(nblk), has_tail, init, out, static_cast<unsigned>(nsh),
-                     static_cast<unsigned>(nsh_stripe), static_cast<unsigned>(x0_shard), x0_src);
+                     static_cast<unsigned>(nblk), has_tail, init, out, static_cast<unsigned>(nsh));
   isal_hip_count_launch();
   return static_cast<int>(hipGetLastError());
 }

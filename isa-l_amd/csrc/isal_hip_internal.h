@@ -73,10 +73,10 @@ unsigned long long isal_hip_run(int op, int len, int k, int rows, int vec_i,
 
 /* Parity rows of a pass whose coefficients are all 0 or 1 (RS Vandermonde row
  * 0, RAID P): such a row is the XOR of some sources, so — CRC being
- * GF(2)-linear in the data — its raw CRC partials are the XOR of those
- * sources' partials. The fused encode+CRC kernels skip checksumming row 0 when
- * it is such a row (bit 0 of rows; a compile-time kernel variant) and the
- * combine kernels derive it. rows: bit l set for such a row l <
+ * GF(2)-linear in the data — its raw CRC chains are the XOR of those sources'
+ * chains. The fused encode+CRC kernels do not checksum row 0 when it is such
+ * a row (bit 0 of rows; a compile-time kernel variant): they form its chains
+ * from the source chains once per block. rows: bit l set for such a row l <
  * EC_MAX_ROWS_PER_PASS (k <= 64); src[l]: bit j set where c[l][j] == 1. */
 typedef struct {
         unsigned rows;
@@ -237,14 +237,10 @@ int isal_hip_launch_encode_crc(const uint64_t *d_ptrs, int ptr_stride, int src_i
                                const uint32_t *d_tbl, const isal_hip_xrows *xr, int len, int k,
                                int rows, long long nstripes, int tt, const uint32_t *d_tabs,
                                uint32_t *d_part, uint32_t *d_tail, void *stream);
-/* out[sh] = crc32_iscsi of shard sh (sh < nsh, nsh_stripe shards per stripe)
- * from its partials. x0_src != 0: shard x0_shard of each stripe (row 0 of a
- * fused encode under X0) is derived as the XOR of the partials of the source
- * shards in the x0_src mask. */
+/* out[sh] = crc32_iscsi of shard sh (sh < nsh) from its partials. */
 int isal_hip_launch_crc_combine(const uint32_t *d_part, const uint32_t *d_tail,
                                 const uint32_t *d_plan, long long nblk, int has_tail,
-                                unsigned int init, uint32_t *out, long long nsh, int nsh_stripe,
-                                int x0_shard, unsigned long long x0_src, void *stream);
+                                unsigned int init, uint32_t *out, long long nsh, void *stream);
 
 #ifdef __cplusplus
 }

@@ -995,15 +995,13 @@ batch_crc_setup(isal_hip_batch *b)
         return ISAL_HIP_OK;
 }
 
-/* x0: the fused kernel left parity row 0 to be derived (isal_hip_xrows) */
 static int
-batch_crc_finish(isal_hip_batch *b, unsigned int init, unsigned int *crc, int x0, void *stream)
+batch_crc_finish(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
 {
         const long long nsh = (long long) b->nstripes * (b->k + b->rows);
         return isal_hip_launch_crc_combine(b->d_part, b->d_tail, b->d_crc + ISAL_HIP_CRC_TAB_DWORDS,
                                            b->crc.nblk, b->crc.tail != 0, init, (uint32_t *) crc,
-                                           nsh, b->k + b->rows, b->k,
-                                           x0 ? b->xr.src[0] : 0ull, stream)
+                                           nsh, stream)
                        ? ISAL_HIP_EHIP
                        : ISAL_HIP_OK;
 }
@@ -1033,7 +1031,7 @@ isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void
                                 b->vec16, b->crc.tt, b->d_crc, b->d_part, b->d_tail,
                                 b->k + b->rows, 0, stream))
                 return ISAL_HIP_EHIP;
-        return batch_crc_finish(b, init, crc, 0, stream);
+        return batch_crc_finish(b, init, crc, stream);
 }
 
 /* ---- CRC64 of the batch's shards (isal_hip.h) ----------------------------- */
@@ -1128,7 +1126,7 @@ isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long i
 int
 isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
 {
-        int r, x0 = 0;
+        int r;
         if (!b || !crc)
                 return ISAL_HIP_EINVAL;
         if (b->len == 0)
@@ -1137,12 +1135,11 @@ isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *cr
                 return r;
         if (b->vec16 && b->len % 16 == 0 && b->k >= 1 && b->k <= ISAL_HIP_CRC_MAX_FUSED_K) {
                 /* one pass over the stripe: encode + CRC of all k + rows shards
-                 * (row 0 derived from the sources when it is a 0/1 row) */
+                 * (row 0's chains formed from the sources' when it is a 0/1 row) */
                 if (isal_hip_launch_encode_crc(b->d_ptrs, b->k + b->rows, 0, b->k, b->d_tbl, &b->xr,
                                                b->len, b->k, b->rows, b->nstripes, b->crc.tt,
                                                b->d_crc, b->d_part, b->d_tail, stream))
                         return ISAL_HIP_EHIP;
-                x0 = b->xr.rows & 1u;
         } else {
                 /* unaligned shards, ragged len or very wide k: encode, then CRC */
                 if (isal_hip_batch_encode(b, stream) != ISAL_HIP_OK)
@@ -1152,5 +1149,5 @@ isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *cr
                                         b->d_tail, b->k + b->rows, 0, stream))
                         return ISAL_HIP_EHIP;
         }
-        return batch_crc_finish(b, init, crc, x0, stream);
+        return batch_crc_finish(b, init, crc, stream);
 }

@@ -381,7 +381,9 @@ def test_hip_failure_falls_back_to_cpu_route(engine, oracle, gpu, monkeypatch, s
         for v in rng.permutation(k):
             engine.ec_encode_data_update(n, k, rows, int(v), tbls, src[int(v)], upd)
         assert all(np.array_equal(a, b) for a, b in zip(upd, want)), ("update", site, n)
-        assert engine.fallbacks() > before, (site, n)
+        zero_copy = n == 4096  # the kernel reads/writes pinned memory: no H2D / D2H copies
+        if not (zero_copy and site in (2, 4)):
+            assert engine.fallbacks() > before, (site, n)
 
 
 def test_dropin_call_ordered_after_default_stream_work(engine, oracle, gpu):
@@ -630,17 +632,20 @@ def test_encode_crc_tiles_per_workgroup(engine, oracle, gpu, monkeypatch, k, row
     b.close()
 
 
+@pytest.mark.parametrize("chain", ["lds", "reg"])
 @pytest.mark.parametrize("xrows", ["1", "0"])
 @pytest.mark.parametrize("k,n,tt", [(10, 4096 * 37 + 2048, 4), (7, 65536, None), (10, 65536, None)])
-def test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, xrows, k, n, tt):
-    """Parity rows whose coefficients are all 0/1 (all-ones, RAID-P-like rows
-    with zeros, an all-zero row) get their CRC32C / CRC64 from the sources'
-    partials instead of being checksummed (ISAL_HIP_CRC_XROWS=1, default);
-    both ways every CRC == the oracle, full and ragged tiles, register and
-    LDS source chains."""
+def test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, chain, xrows, k, n, tt):
+    """A parity row 0 whose coefficients are all 0/1 gets its CRC32C / CRC64
+    chains from the sources' chains instead of being checksummed
+    (ISAL_HIP_CRC_XROWS=1, default; other 0/1 rows, an all-zero row and a
+    general row are checksummed); both ways every CRC == the oracle, full and
+    ragged tiles, register and LDS source chains."""
     import torch
 
     _setenv(monkeypatch, "ISAL_HIP_CRC_XROWS", xrows)
+    _setenv(monkeypatch, "ISAL_HIP_CRC_SRC_CHAIN", chain)    # CRC32C source chains
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_SRC_CHAIN", chain)  # CRC64 source chains
     if tt:
         _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
     rows, ns = 5, 3
