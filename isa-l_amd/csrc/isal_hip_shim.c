@@ -943,14 +943,16 @@ isal_hip_batch_destroy(isal_hip_batch *b)
 
 /* ---- CRC32C of the batch's shards (isal_hip.h) ---------------------------- */
 
-/* Tiles per CRC workgroup: 16 (64 KiB of each shard, partials = 0.4 % of the
- * bytes), halved while the launch would have fewer than 2048 workgroups. */
+/* Tiles per CRC workgroup: `def` (CRC32C 16: 64 KiB of each shard, partials
+ * 0.4 % of the bytes; CRC64 32: fewer blocks for the combine's Horner steps —
+ * C2 sweep, profiles/r02_crc_tile_sweep.txt), halved while the launch would
+ * have fewer than 2048 workgroups. ISAL_HIP_CRC_TILES overrides. */
 static int
-crc_tiles(int len, int nstripes)
+crc_tiles(int len, int nstripes, int def)
 {
         const long long knob = isal_hip_knob(ISAL_HIP_KNOB_CRC_TILES);
         long long ntiles = ((long long) len + ISAL_HIP_CRC_TILE - 1) / ISAL_HIP_CRC_TILE;
-        int tt = knob >= 0 ? (int) knob : 16;
+        int tt = knob >= 0 ? (int) knob : def;
         if (tt < 1)
                 tt = 1;
         if (knob >= 0)
@@ -969,7 +971,7 @@ batch_crc_setup(isal_hip_batch *b)
         hipError_t e;
         if (b->d_crc)
                 return ISAL_HIP_OK;
-        isal_hip_crc_geometry(b->len, crc_tiles(b->len, b->nstripes), &b->crc);
+        isal_hip_crc_geometry(b->len, crc_tiles(b->len, b->nstripes, 16), &b->crc);
         nsh = (size_t) b->nstripes * (size_t) (b->k + b->rows);
         part = nsh * (size_t) b->crc.nblk * 256;
         tail = nsh * 256;
@@ -1046,7 +1048,7 @@ batch_crc64_setup(isal_hip_batch *b, int variant)
         if (b->d_c64tab[variant])
                 return ISAL_HIP_OK;
         if (!b->d_c64part && !b->c64_tt) {
-                b->c64_tt = crc_tiles(b->len, b->nstripes);
+                b->c64_tt = crc_tiles(b->len, b->nstripes, 32);
                 isal_hip_crc64_geometry(b->len, b->c64_tt, &g);
                 if (g.nblk) {
                         e = hipMalloc((void **) &b->d_c64part, (size_t) b->nstripes *

@@ -152,6 +152,13 @@ for s in $STEPS; do
                         run bench_$wl 300 python bench.py --workload $wl --no-cpu-baseline
                 done
                 ;;
+        ttsweep)
+                for tt in ${TT_LIST:-8 16 32 64}; do
+                        for wl in encode-crc64 encode-crc crc64; do
+                                ISAL_HIP_CRC_TILES=$tt run bench_${wl}_tt$tt 300 python bench.py --workload $wl --no-cpu-baseline
+                        done
+                done
+                ;;
         e2etrace)
                 for dp in 2 6; do
                         run e2etrace_d$dp 300 rocprofv3 --memory-copy-trace --kernel-trace --stats --output-format csv -d "$OUT/e2etrace_d$dp" -o t -- python3 bench.py --workload e2e-encode --steps 100 --warmup 10 --depth $dp
