@@ -17,9 +17,15 @@
  * raid_base.c:70-140): only byte 1 of each 32-byte gftbls entry — the
  * coefficient c — is read, exactly like the reference's base functions, so
  * the answer is the reference's for ANY gftbls. The arithmetic is written
- * fresh for this route: c*x = lo_c[x & 15] ^ hi_c[x >> 4] with 16-entry nibble
- * product tables derived from c (GF(2)-linearity), evaluated 32 columns at a
- * time with AVX2 byte shuffles when the CPU has AVX2, else per byte.
+ * fresh for this route, in three widths picked by what the CPU has:
+ *   - GFNI + AVX-512: c*x is the GF(2)-linear map x -> A_c x with A_c the 8x8
+ *     bit matrix whose column j is c*2^j; vgf2p8affineqb applies it to 64
+ *     bytes at once (the reference's fastest kernels do the same,
+ *     gf_vect_gfni.inc:34-72); tails use masked loads/stores;
+ *   - AVX2: c*x = lo_c[x & 15] ^ hi_c[x >> 4] with 16-entry nibble product
+ *     tables, 32 columns per vpshufb pair;
+ *   - per byte with the same nibble tables.
+ * ISAL_HIP_CPU_SIMD = 2 / 1 / 0 caps the width (tests run all three).
  */
 #include <immintrin.h>
 #include <stdint.h>
@@ -32,6 +38,7 @@
 typedef struct {
         uint8_t lo[16]; /* c * {0x00 .. 0x0f} */
         uint8_t hi[16]; /* c * {0x00, 0x10 .. 0xf0} */
+        uint64_t aff;   /* A_c for vgf2p8affineqb: byte 7-i, bit j = bit i of c*2^j */
 } nib_t;
 
 #define BLOCK 4096 /* columns per block: a block of every source stays in L1/L2 */
@@ -52,6 +59,22 @@ nib_tables(unsigned char c, nib_t *t)
                 b = __builtin_ctz((unsigned) i);
                 t->lo[i] = (uint8_t) (t->lo[i & (i - 1)] ^ p[b]);
                 t->hi[i] = (uint8_t) (t->hi[i & (i - 1)] ^ p[b + 4]);
+        }
+        t->aff = 0; /* filled by aff_matrix() when the GFNI path runs */
+}
+
+/* A_c from the column images c*2^b already in the nibble tables (lo[1 << b],
+ * hi[1 << (b - 4)]): a bit-matrix transpose, only for the GFNI path. */
+static void
+aff_matrix(nib_t *t)
+{
+        int b, i;
+        t->aff = 0;
+        for (b = 0; b < 8; b++) { /* column b: the image c*2^b of input bit b */
+                const uint8_t img = b < 4 ? t->lo[1 << b] : t->hi[1 << (b - 4)];
+                for (i = 0; i < 8; i++) /* output bit i lives in byte 7 - i */
+                        if ((img >> i) & 1)
+                                t->aff |= (uint64_t) 1 << (8 * (7 - i) + b);
         }
 }
 
@@ -195,13 +218,104 @@ mad_avx2(long long a, long long b, int rows, const nib_t *T, const unsigned char
                 mad_scalar(i, b, rows, T, src, dst);
 }
 
-static int
-cpu_has_avx2(void)
+/* ---- GFNI + AVX-512: 64 columns per step ---------------------------------- */
+
+#define GFNI __attribute__((target("avx512f,avx512bw,gfni")))
+#define GFNI_MIN_COLUMNS 4096 /* shorter calls use the AVX2 path (see isal_cpu_run) */
+
+static inline GFNI __attribute__((always_inline)) __mmask64
+cols_mask(long long n)
 {
-        static int v = -1;
-        if (v < 0)
-                v = __builtin_cpu_supports("avx2") ? 1 : 0;
-        return v && isal_hip_knob(ISAL_HIP_KNOB_CPU_SIMD) != 0;
+        return n >= 64 ? ~(__mmask64) 0 : (((__mmask64) 1 << n) - 1);
+}
+
+static inline GFNI __attribute__((always_inline)) unsigned long long
+group_gfni_g(long long a, long long b, int k, int r0, const int G, const nib_t *T,
+             unsigned char *const *src, unsigned char *const *dst, int verify)
+{
+        long long i;
+        int j, n;
+        for (i = a; i < b; i += 64) {
+                const __mmask64 m = cols_mask(b - i); /* masked-off bytes are never touched */
+                __m512i acc[GROUP];
+                for (n = 0; n < G; n++)
+                        acc[n] = _mm512_setzero_si512();
+                for (j = 0; j < k; j++) {
+                        const __m512i x = _mm512_maskz_loadu_epi8(m, src[j] + i);
+                        for (n = 0; n < G; n++)
+                                acc[n] = _mm512_xor_si512(
+                                        acc[n], _mm512_gf2p8affine_epi64_epi8(
+                                                        x, _mm512_set1_epi64((long long) T[n * k + j].aff), 0));
+                }
+                if (!verify) {
+                        for (n = 0; n < G; n++)
+                                _mm512_mask_storeu_epi8(dst[r0 + n] + i, m, acc[n]);
+                } else {
+                        unsigned long long best = ~0ull;
+                        for (n = 0; n < G; n++) {
+                                const __m512i d = _mm512_maskz_loadu_epi8(m, dst[r0 + n] + i);
+                                const __mmask64 ne = _mm512_mask_cmpneq_epi8_mask(m, d, acc[n]);
+                                if (ne) {
+                                        const unsigned long long key = mkey(i + __builtin_ctzll(ne), r0 + n);
+                                        if (key < best)
+                                                best = key;
+                                }
+                        }
+                        if (best != ~0ull)
+                                return best;
+                }
+        }
+        return ~0ull;
+}
+
+static GFNI unsigned long long
+group_gfni(long long a, long long b, int k, int r0, int G, const nib_t *T,
+           unsigned char *const *src, unsigned char *const *dst, int verify)
+{
+        switch (G) {
+        case 1:
+                return group_gfni_g(a, b, k, r0, 1, T, src, dst, verify);
+        case 2:
+                return group_gfni_g(a, b, k, r0, 2, T, src, dst, verify);
+        case 3:
+                return group_gfni_g(a, b, k, r0, 3, T, src, dst, verify);
+        default:
+                return group_gfni_g(a, b, k, r0, GROUP, T, src, dst, verify);
+        }
+}
+
+static GFNI void
+mad_gfni(long long a, long long b, int rows, const nib_t *T, const unsigned char *src,
+         unsigned char *const *dst)
+{
+        long long i;
+        int l;
+        for (i = a; i < b; i += 64) {
+                const __mmask64 m = cols_mask(b - i);
+                const __m512i x = _mm512_maskz_loadu_epi8(m, src + i);
+                for (l = 0; l < rows; l++) {
+                        const __m512i d = _mm512_maskz_loadu_epi8(m, dst[l] + i);
+                        _mm512_mask_storeu_epi8(dst[l] + i, m,
+                                                _mm512_xor_si512(d, _mm512_gf2p8affine_epi64_epi8(
+                                                                            x, _mm512_set1_epi64((long long) T[l].aff), 0)));
+                }
+        }
+}
+
+enum { SIMD_NONE = 0, SIMD_AVX2 = 1, SIMD_GFNI = 2 };
+
+/* Widest path this CPU has, capped by ISAL_HIP_CPU_SIMD (0 / 1 / 2). */
+static int
+cpu_simd(void)
+{
+        static int have = -1;
+        long long cap;
+        if (have < 0)
+                have = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("gfni")
+                               ? SIMD_GFNI
+                               : __builtin_cpu_supports("avx2") ? SIMD_AVX2 : SIMD_NONE;
+        cap = isal_hip_knob(ISAL_HIP_KNOB_CPU_SIMD);
+        return cap >= 0 && cap < have ? (int) cap : have;
 }
 
 /* ---- entry ---------------------------------------------------------------- */
@@ -210,7 +324,14 @@ unsigned long long
 isal_cpu_run(int op, long long c0, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
              unsigned char *const *src, int nsrc, unsigned char *const *dst)
 {
-        const int avx2 = cpu_has_avx2();
+        /* short calls stay on 256-bit code: on the container's Xeon the first
+         * 512-bit instructions of a burst of tiny calls cost more than they
+         * save (xor_check_test: 16 s AVX2, 30 s GFNI) */
+        const int simd0 = cpu_simd();
+        const int simd = simd0 == SIMD_GFNI && (long long) len - c0 < GFNI_MIN_COLUMNS
+                                 && isal_hip_knob(ISAL_HIP_KNOB_CPU_SIMD) != SIMD_GFNI
+                         ? SIMD_AVX2
+                         : simd0;
         const int ncoef = op == ISAL_HIP_OP_UPDATE ? rows : rows * k;
         nib_t stack_tab[64], *T;
         unsigned long long best = ~0ull;
@@ -225,11 +346,16 @@ isal_cpu_run(int op, long long c0, int len, int k, int rows, int vec_i, const un
 
         if (op == ISAL_HIP_OP_UPDATE) {
                 /* dst[l] ^= c[l][vec_i] * src (ec_base.c:327-342) */
-                for (l = 0; l < rows; l++)
+                for (l = 0; l < rows; l++) {
                         nib_tables(gftbls[((size_t) l * k + vec_i) * 32 + 1], &T[l]);
+                        if (simd == SIMD_GFNI)
+                                aff_matrix(&T[l]);
+                }
                 for (a = c0; a < len; a += BLOCK) {
                         const long long b = len - a < BLOCK ? len : a + BLOCK;
-                        if (avx2)
+                        if (simd == SIMD_GFNI)
+                                mad_gfni(a, b, rows, T, src[0], dst);
+                        else if (simd == SIMD_AVX2)
                                 mad_avx2(a, b, rows, T, src[0], dst);
                         else
                                 mad_scalar(a, b, rows, T, src[0], dst);
@@ -239,8 +365,12 @@ isal_cpu_run(int op, long long c0, int len, int k, int rows, int vec_i, const un
                 const int verify = op == ISAL_HIP_OP_VERIFY;
                 (void) nsrc;
                 for (l = 0; l < rows; l++)
-                        for (j = 0; j < k; j++)
-                                nib_tables(gftbls[((size_t) l * k + j) * 32 + 1], &T[(size_t) l * k + j]);
+                        for (j = 0; j < k; j++) {
+                                nib_t *tj = &T[(size_t) l * k + j];
+                                nib_tables(gftbls[((size_t) l * k + j) * 32 + 1], tj);
+                                if (simd == SIMD_GFNI)
+                                        aff_matrix(tj);
+                        }
                 for (a = c0; a < len && best == ~0ull; a += BLOCK) {
                         const long long b = len - a < BLOCK ? len : a + BLOCK;
                         int r0;
@@ -263,8 +393,9 @@ isal_cpu_run(int op, long long c0, int len, int k, int rows, int vec_i, const un
                                         }
                                         continue;
                                 }
-                                key = avx2 ? group_avx2(a, b, k, r0, G, Tg, src, dst, verify)
-                                           : group_scalar(a, b, k, r0, G, Tg, src, dst, verify);
+                                key = simd == SIMD_GFNI ? group_gfni(a, b, k, r0, G, Tg, src, dst, verify)
+                                      : simd == SIMD_AVX2 ? group_avx2(a, b, k, r0, G, Tg, src, dst, verify)
+                                                          : group_scalar(a, b, k, r0, G, Tg, src, dst, verify);
                                 if (key < best)
                                         best = key;
                         }

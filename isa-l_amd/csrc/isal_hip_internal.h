@@ -92,7 +92,7 @@ enum {
         ISAL_HIP_KNOB_BACKEND,       /* auto(0) | gpu(1) | cpu(2); -2 = unknown word */
         ISAL_HIP_KNOB_CPU_MAX_BYTES, /* auto route: host calls up to this many bytes run on the CPU */
         ISAL_HIP_KNOB_LOG,           /* 1: log every drop-in call's route to stderr */
-        ISAL_HIP_KNOB_CPU_SIMD,      /* 0: CPU route without AVX2 (per-byte; tests) */
+        ISAL_HIP_KNOB_CPU_SIMD,      /* CPU route width cap: 0 per byte, 1 AVX2, 2 GFNI (tests) */
         ISAL_HIP_KNOB_STAGE_MB,
         ISAL_HIP_KNOB_GRID_CAP,
         ISAL_HIP_KNOB_CRC_TILES,

@@ -6,8 +6,8 @@ Checked like the GPU path: against the reference's own outputs
 (tests/golden, generated from /root/reference ec_base.c / raid_base.c), the
 oracle on random shapes, the reference's contracts (padding untouched,
 update == encode, RAID check positions) and the reference's own test
-programs linked against libisal_hip.so. Both the AVX2 and the per-byte
-variants run. No GPU needed: ISAL_HIP_BACKEND=cpu pins the route either way.
+programs linked against libisal_hip.so. The GFNI (AVX-512), AVX2 and per-byte
+variants all run. No GPU needed: ISAL_HIP_BACKEND=cpu pins the route either way.
 """
 import os
 import subprocess
@@ -19,13 +19,12 @@ import ecutil
 from ecutil import coeffs, fill_bytes, golden
 
 
-@pytest.fixture(params=["avx2", "scalar"])
+@pytest.fixture(params=["gfni", "avx2", "scalar"])
 def cpu_engine(engine, request, monkeypatch):
+    """The CPU route at each width (capped by ISAL_HIP_CPU_SIMD; a CPU without
+    GFNI / AVX2 runs the next narrower path, still checked)."""
     monkeypatch.setenv("ISAL_HIP_BACKEND", "cpu")
-    if request.param == "scalar":
-        monkeypatch.setenv("ISAL_HIP_CPU_SIMD", "0")
-    else:
-        monkeypatch.delenv("ISAL_HIP_CPU_SIMD", raising=False)
+    monkeypatch.setenv("ISAL_HIP_CPU_SIMD", {"gfni": "2", "avx2": "1", "scalar": "0"}[request.param])
     engine.reload_config()
     launches, calls = engine.kernel_launches(), engine.cpu_calls()
     yield engine
