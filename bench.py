@@ -645,7 +645,8 @@ def main(argv=None):
                 u = enc_group(k)  # one load group (k == U): source CRC chains in registers
                 reg = k == u and os.environ.get("ISAL_HIP_CRC_SRC_CHAIN") == "reg"
                 x0 = "false" if reg else "true"  # Vandermonde row 0 derived (LDS-chain variant)
-                kernel = f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true, {x0}>"
+                nb = 0 if reg or os.environ.get("ISAL_HIP_CRC_BYTE_DWORDS") == "0" else 4  # byte tables
+                kernel = f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true, {x0}, {nb}>"
                 workload = (f"C2 encode + CRC32C (crc32_iscsi) of all k+p shards in one pass: k={k} "
                             f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
             else:
@@ -659,7 +660,18 @@ def main(argv=None):
             bytes_per_launch = (k + p) * n * S
             u = enc_group(k)
             reg = k == u and os.environ.get("ISAL_HIP_CRC64_SRC_CHAIN") == "reg"
-            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(reg).lower()}, true>"  # X0: Vandermonde row 0 derived
+            sl = os.environ.get("ISAL_HIP_CRC64_SLICE") != "0"  # slicing-by-8 chunk path (default)
+            # lane groups per workgroup: the launcher's rule (crc64_kernels.hip fused_nv)
+            tabs_b, la_b, cap = (4992 if sl else 2688) * 8, k * 256 * 8, 160 * 1024
+            nv_env = os.environ.get("ISAL_HIP_CRC64_FUSED_NV")
+            if reg or tabs_b + 2 * la_b > cap:
+                nv = 1
+            elif nv_env in ("1", "2"):
+                nv = int(nv_env)
+            else:
+                nv = 2 if 2 * (cap // (tabs_b + 2 * la_b)) > cap // (tabs_b + la_b) else 1
+            # X0: Vandermonde row 0 derived
+            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(reg).lower()}, true, {str(sl).lower()}, {nv}>"
             workload = (f"C2 encode + CRC64 (crc64_ecma_refl) of all k+p shards in one pass: k={k} "
                         f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
         elif args.workload == "crc64":

@@ -162,6 +162,44 @@ chunk_tables(const uint64_t basis[128], uint64_t *out)
                         }
 }
 
+/* The u-domain of the slicing path: u = pi(s), pi = byte swap for the norm
+ * flavours. Processing 8 data bytes d (little-endian word) from register s is
+ * raw(s, d) = raw(0, d ^ s) (refl: the register is XORed into the low bytes)
+ * or raw(0, d ^ bswap(s)) (norm: into the high bytes, first byte = bits
+ * 56..63), i.e. raw(0, d ^ pi(s)) — so in u the update is u' = A(d ^ u) with
+ * A = pi o raw(0, .) for every flavour, and a 16-byte chunk is two such steps. */
+static uint64_t
+pi_of(int variant, uint64_t x)
+{
+        return isal_hip_crc64_is_refl(variant) ? x : __builtin_bswap64(x);
+}
+
+static void
+slice_tables(int variant, uint64_t *tabs)
+{
+        uint64_t z[64], zu[64];
+        uint8_t d[8];
+        int j, v, i, s;
+        uint64_t *a = tabs + ISAL_HIP_CRC64_SLICE_TAB, *b = a + 8 * 256;
+        isal_hip_crc64_zpow(variant, ISAL_HIP_CRC_TILE, z);
+        for (j = 0; j < 8; j++)
+                for (v = 0; v < 256; v++) {
+                        uint64_t r;
+                        memset(d, 0, sizeof(d));
+                        d[j] = (uint8_t) v;
+                        r = raw_update(variant, 0, d, 8);
+                        a[j * 256 + v] = pi_of(variant, r);
+                        b[j * 256 + v] = pi_of(variant, apply(z, r));
+                }
+        /* pi Z^(4096 s) pi as field tables, s = 1, 2 */
+        for (s = 1; s <= 2; s++) {
+                isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * s, z);
+                for (i = 0; i < 64; i++)
+                        zu[i] = pi_of(variant, apply(z, pi_of(variant, 1ULL << i)));
+                op_tables(zu, tabs + ISAL_HIP_CRC64_UOP_TAB + (s - 1) * ISAL_HIP_CRC64_OP_ENTRIES);
+        }
+}
+
 /* Layout: isal_hip_internal.h (ISAL_HIP_CRC64_*). */
 void
 isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
@@ -210,6 +248,7 @@ isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
         }
         isal_hip_crc64_zpow(variant, (unsigned long long) (g.tail / 16) * 16, m);
         op_tables(m, tabs + ISAL_HIP_CRC64_OP_TAIL);
+        slice_tables(variant, tabs);
 }
 
 void

@@ -73,7 +73,7 @@ struct X64 {
   }
 };
 
-__device__ __forceinline__ X64 x64(uint64_t v) {
+__device__ __forceinline__ __attribute__((unused)) X64 x64(uint64_t v) {
   return {static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32)};
 }
 
@@ -103,7 +103,7 @@ __device__ __forceinline__ void apply_op_acc(X64& acc, const uint64_t* op, uint6
   lookup14(acc, op, static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
 }
 
-__device__ __forceinline__ uint64_t apply_op(const uint64_t* op, uint64_t v) {
+__device__ __forceinline__ __attribute__((unused)) uint64_t apply_op(const uint64_t* op, uint64_t v) {
   X64 a{0u, 0u};
   apply_op_acc(a, op, v);
   return a.get();
@@ -129,20 +129,23 @@ __device__ __forceinline__ uint32_t le32(const uint8_t* p) {
 }
 
 // raw(0, 16 bytes at base + off) with byte loads (any alignment).
-__device__ __forceinline__ uint64_t chunk_crc_bytes(const uint64_t* t, uint64_t base, long long off) {
+__device__ __forceinline__ __attribute__((unused)) uint64_t chunk_crc_bytes(const uint64_t* t, uint64_t base,
+                                                                           long long off) {
   const uint8_t* p = reinterpret_cast<const uint8_t*>(base) + off;
   return chunk_crc(t, le32(p), le32(p + 4), le32(p + 8), le32(p + 12));
 }
 
-template <int N>
+template <int N, int NV = 1>
 __device__ __forceinline__ void load_lds(uint64_t* dst, const uint64_t* __restrict__ src) {
   const uint4* s = reinterpret_cast<const uint4*>(src);
   uint4* d = reinterpret_cast<uint4*>(dst);
-  for (int i = threadIdx.x; i < N / 2; i += kBlock) d[i] = s[i];
+  for (int i = threadIdx.x; i < N / 2; i += kBlock * NV) d[i] = s[i];
 }
 
-constexpr int kBatch = 4;  // full tiles whose loads are issued together (default)
+[[maybe_unused]] constexpr int kBatch = 4;  // full tiles whose loads are issued together (default)
 constexpr int kCE = ISAL_HIP_CRC64_CHUNK_ENTRIES;
+
+#ifndef ISAL_FUSED64_PART  // standalone kernels: the main object only
 
 // LDS layout of crc64_shards<VEC, M>: chunk map (m = 0) and Z^4096 [kKernTab],
 // the chunk maps followed by m = 1..M-1 tiles, Z^(4096*M).
@@ -304,6 +307,8 @@ int load_batch() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC64_BATCH) == 8 ? 8 : 4;
 }
 
+#else  // ISAL_FUSED64_PART: one object per parity-row count P (parallel build)
+
 // ---------------------------------------------------------------------------
 // Fused encode + CRC64 (the fragment checksum in the
 // encode pass). The encode half is ec_encode_v16's GF arithmetic on the same
@@ -361,6 +366,58 @@ __device__ __forceinline__ uint64_t chain_step(const uint64_t* lt, uint64_t a, u
   return c.get();
 }
 
+// ---- slicing-by-8 chunk path of the fused kernel (SL) ----------------------
+// The field-table path costs ~1.7 VALU per 5-bit field offset + 1 per 64-bit
+// fold, 28 lookups per 16-byte chunk, and the fused kernel is VALU-issue-bound
+// (DESIGN §3). Here a chunk is two slicing-by-8 steps in the u-domain
+// (crc64_host.c: u = pi(s), one update rule for every flavour):
+//   u1 = A(lo8),  raw_u(chunk) = A(hi8 ^ u1),  T1_u(chunk) = B(hi8 ^ u1)
+// 16 byte-indexed lookups, each offset one SDWA shift (byte select + << 3).
+// The 256-entry tables are not bank-conflict-free (8 entries per bank pair):
+// this trades VALU issue for LDS cycles.
+constexpr int kSA = 0, kSB = 8 * 256, kSZ1 = 16 * 256, kSZ2 = kSZ1 + kOp;
+constexpr int kSlLds = kSZ2 + kOp;
+
+// Byte b of w times 8 (an 8-byte entry's offset) in one VALU op.
+__device__ __forceinline__ void byte_offs8(uint32_t w, uint32_t (&o)[4]) {
+  const uint32_t three = 3;
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+      : "=v"(o[0]) : "v"(three), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+      : "=v"(o[1]) : "v"(three), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+      : "=v"(o[2]) : "v"(three), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+      : "=v"(o[3]) : "v"(three), "v"(w));
+}
+
+__device__ __forceinline__ uint64_t tab8_at(const uint64_t* t, int j, uint32_t o) {
+  return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(t) + j * 2048 + o);
+}
+
+// acc ^= S(lo | hi << 32) for the slicing table set S at t (8 tables of 256).
+__device__ __forceinline__ void slice8_acc(X64& acc, const uint64_t* t, uint32_t lo, uint32_t hi) {
+  uint32_t o[4], q[4];
+  byte_offs8(lo, o);
+  byte_offs8(hi, q);
+  acc.add2(tab8_at(t, 0, o[0]), tab8_at(t, 1, o[1]));
+  acc.add2(tab8_at(t, 2, o[2]), tab8_at(t, 3, o[3]));
+  acc.add2(tab8_at(t, 4, q[0]), tab8_at(t, 5, q[1]));
+  acc.add2(tab8_at(t, 6, q[2]), tab8_at(t, 7, q[3]));
+}
+
+// chain_step in the u-domain through the slicing tables.
+template <int PH>
+__device__ __forceinline__ uint64_t chain_step_sl(const uint64_t* lt, uint64_t a, uint32_t w0,
+                                                  uint32_t w1, uint32_t w2, uint32_t w3) {
+  X64 u{0u, 0u};
+  slice8_acc(u, lt + kSA, w0, w1);
+  X64 c = PH == 2 ? x64(a) : X64{0u, 0u};
+  if constexpr (PH != 2) apply_op_acc(c, lt + (PH == 1 ? kSZ2 : kSZ1), a);
+  slice8_acc(c, lt + (PH == 1 ? kSB : kSA), w2 ^ u.lo, w3 ^ u.hi);
+  return c.get();
+}
+
 template <int P, int U, bool REG>
 constexpr int fused64_waves() {
   constexpr int est = (4 * U * (REG ? 2 : 1) + 6 * P + (REG ? 2 * U : 0) + 88 + 7) / 8 * 8;
@@ -373,20 +430,42 @@ constexpr int fused64_waves() {
 // chain is not computed per tile but formed once per block from those
 // sources' chains. A compile-time variant: a runtime row mask in the tile
 // loop costs registers.
-template <int P, int U, bool REG, bool X0 = false>
-__global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encode_crc64_v16(
+// SL: chunks through the slicing tables, chains in the u-domain; uswap (norm
+// flavours) turns them back into registers (u = bswap(s)) before they are stored.
+// NV: independent 256-lane groups per workgroup. They share one LDS copy of the
+// tables (each works its own items, no barrier after the table load), so the
+// per-lane source chains, not the tables, set how many waves fit a CU.
+template <int P, int U, bool REG, bool X0 = false, bool SL = false, int NV = 1>
+__global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_encode_crc64_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, const uint32_t* __restrict__ tbl, int len,
     int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged, int pair,
-    unsigned long long x0src, const uint64_t* __restrict__ tabs, uint64_t* __restrict__ part) {
-  __shared__ uint64_t lt[kKernTab + kCE + kOp];
-  extern __shared__ uint64_t la[];  // [k][kBlock] source chains when !REG
-  load_lds<kKernTab>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
-  load_lds<kCE>(lt + kT1, tabs + ISAL_HIP_CRC64_CHUNKX_TAB);
-  load_lds<kOp>(lt + kZ2, tabs + ISAL_HIP_CRC64_SHIFTX_TAB);
+    unsigned long long x0src, int uswap, const uint64_t* __restrict__ tabs,
+    uint64_t* __restrict__ part) {
+  __shared__ uint64_t lt[SL ? kSlLds : kKernTab + kCE + kOp];
+  extern __shared__ uint64_t la[];  // [k][kBlock * NV] source chains when !REG
+  if constexpr (SL) {
+    load_lds<kSlLds, NV>(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB);  // SLICE and UOP are contiguous
+  } else {
+    load_lds<kKernTab, NV>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
+    load_lds<kCE, NV>(lt + kT1, tabs + ISAL_HIP_CRC64_CHUNKX_TAB);
+    load_lds<kOp, NV>(lt + kZ2, tabs + ISAL_HIP_CRC64_SHIFTX_TAB);
+  }
+  constexpr int kLa = kBlock * NV;           // source-chain row stride
+  const unsigned tid = threadIdx.x % kBlock;  // lane within its group
   __syncthreads();
+  auto step = [&](auto phc, uint64_t a, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
+                  __attribute__((always_inline)) {
+    if constexpr (SL)
+      return chain_step_sl<decltype(phc)::value>(lt, a, w0, w1, w2, w3);
+    else
+      return chain_step<decltype(phc)::value>(lt, a, w0, w1, w2, w3);
+  };
+  auto to_reg = [&](uint64_t v) __attribute__((always_inline)) {
+    return SL && uswap ? __builtin_bswap64(v) : v;
+  };
   const int nsh = k + P;
-  const long long lane = threadIdx.x * kVec;
-  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+  const long long lane = tid * kVec;
+  for (unsigned w = blockIdx.x * NV + threadIdx.x / kBlock; w < nitems; w += gridDim.x * NV) {
     const unsigned stripe = w / nblk, blk = w - stripe * nblk;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const unsigned t0 = blk * tt, t1 = t0 + tt < nfull ? t0 + tt : nfull;
@@ -396,7 +475,7 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
 #pragma unroll
     for (int j = 0; j < (REG ? U : 1); ++j) ra[j] = 0;
     if constexpr (!REG)
-      for (int j = 0; j < k; ++j) la[j * kBlock + threadIdx.x] = 0;
+      for (int j = 0; j < k; ++j) la[j * kLa + threadIdx.x] = 0;
     // Chain phase of a tile (uniform across the workgroup, a template
     // argument of the tile body). With pair, tiles go in pairs: the even tile
     // applies a = Z^8192(a) ^ T1(chunk), the odd one a ^= raw(0, chunk) — 70
@@ -415,13 +494,12 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
     };
     auto tile_body = [&](auto phc, uint32_t (&acc)[P][4], long long off, auto&& macs)
                          __attribute__((always_inline)) {
-      constexpr int PH = decltype(phc)::value;
       auto feed = [&](int j, const uint4& x) __attribute__((always_inline)) {
         if constexpr (REG) {
-          ra[j] = chain_step<PH>(lt, ra[j], x.x, x.y, x.z, x.w);
+          ra[j] = step(phc, ra[j], x.x, x.y, x.z, x.w);
         } else {
-          uint64_t* a = la + j * kBlock + threadIdx.x;
-          *a = chain_step<PH>(lt, *a, x.x, x.y, x.z, x.w);
+          uint64_t* a = la + j * kLa + threadIdx.x;
+          *a = step(phc, *a, x.x, x.y, x.z, x.w);
         }
       };
       macs(feed);
@@ -429,7 +507,7 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
       for (int l = 0; l < P; ++l) {
         store16<kNT>(sp[k + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
         if (!(X0 && l == 0))
-          ao[l] = chain_step<PH>(lt, ao[l], acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+          ao[l] = step(phc, ao[l], acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
       }
     };
     if constexpr (REG) {
@@ -498,20 +576,20 @@ __global__ __launch_bounds__(kBlock, (fused64_waves<P, U, REG>())) void ec_encod
           if ((x0src >> j) & 1ull) v ^= ra[j];
       } else {
         for (int j = 0; j < k; ++j)
-          if ((x0src >> j) & 1ull) v ^= la[j * kBlock + threadIdx.x];
+          if ((x0src >> j) & 1ull) v ^= la[j * kLa + threadIdx.x];
       }
       ao[0] = v;
     }
-    uint64_t* pp = part + (static_cast<size_t>(stripe) * nsh * nblk + blk) * kBlock + threadIdx.x;
+    uint64_t* pp = part + (static_cast<size_t>(stripe) * nsh * nblk + blk) * kBlock + tid;
     const size_t sstep = static_cast<size_t>(nblk) * kBlock;
     if constexpr (REG) {
 #pragma unroll
-      for (int j = 0; j < U; ++j) pp[j * sstep] = ra[j];
+      for (int j = 0; j < U; ++j) pp[j * sstep] = to_reg(ra[j]);
     } else {
-      for (int j = 0; j < k; ++j) pp[j * sstep] = la[j * kBlock + threadIdx.x];
+      for (int j = 0; j < k; ++j) pp[j * sstep] = to_reg(la[j * kLa + threadIdx.x]);
     }
 #pragma unroll
-    for (int l = 0; l < P; ++l) pp[(k + l) * sstep] = ao[l];
+    for (int l = 0; l < P; ++l) pp[(k + l) * sstep] = to_reg(ao[l]);
   }
 }
 
@@ -542,39 +620,88 @@ bool src_chain_reg64() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC64_SRC_CHAIN) == 1;  // "reg"
 }
 
+// Slicing-by-8 chunk path in the fused kernel: on by default
+// (ISAL_HIP_CRC64_SLICE=0 selects the field tables). C2 step, LDS chains, two
+// lane groups: 4.58 -> 4.01 ms (VALU 2.40e9 -> 1.83e9 wave-instructions,
+// profiles/r02_fastcrc_*); with register chains (240 VGPRs) it is slower.
+bool slice64() {
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_SLICE) != 0;
+}
+
+// 256-lane groups per workgroup of the LDS-chain fused kernel: the knob
+// (ISAL_HIP_CRC64_FUSED_NV = 1 or 2) or, unset, 2 when that fits more lane
+// groups on a CU (160 KiB of LDS; the static tables are shared by a workgroup,
+// the source chains are per lane).
+int fused_nv(bool sl, int k) {
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_FUSED_NV);
+  const size_t cap = 160 * 1024, tabs = (sl ? kSlLds : kKernTab + kCE + kOp) * 8,
+               la = static_cast<size_t>(k) * kBlock * 8;
+  if (tabs + 2 * la > cap) return 1;
+  if (v == 1 || v == 2) return static_cast<int>(v);
+  return 2 * (cap / (tabs + 2 * la)) > cap / (tabs + la) ? 2 : 1;
+}
+
 template <int P, int U>
 void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
                     const uint32_t* tbl, int len, int k, unsigned nitems,
-                    const isal_hip_crc64_geom& g, const isal_hip_xrows& xr, const uint64_t* tabs,
-                    uint64_t* part) {
+                    const isal_hip_crc64_geom& g, const isal_hip_xrows& xr, int refl,
+                    const uint64_t* tabs, uint64_t* part) {
   const int ragged = g.tail != 0;
-#define FUSED64_LAUNCH(REG, X0, LDS)                                                              \
-  hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, REG, X0>), dim3(grid), dim3(kBlock), LDS, s, ptrs, \
-                     ptr_stride, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),             \
-                     static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), ragged,         \
-                     pair_step(), xr.src[0], tabs, part)
+#define FUSED64_LAUNCH(REG, X0, SL, NV)                                                           \
+  hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, REG, X0, SL, NV>), dim3((grid + NV - 1) / NV),     \
+                     dim3(kBlock * NV), REG ? 0 : lds * NV, s, ptrs, ptr_stride, tbl, len, k,      \
+                     nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),          \
+                     static_cast<unsigned>(g.nfull), ragged, pair_step(), xr.src[0], !refl, tabs, part)
+#define FUSED64_X0(REG, SL, NV)                                                                    \
+  do {                                                                                             \
+    if (xr.rows & 1u) FUSED64_LAUNCH(REG, true, SL, NV); else FUSED64_LAUNCH(REG, false, SL, NV); \
+  } while (0)
   const size_t lds = static_cast<size_t>(k) * kBlock * 8;
-  if (k == U && src_chain_reg64()) {
-    if (xr.rows & 1u) FUSED64_LAUNCH(true, true, 0); else FUSED64_LAUNCH(true, false, 0);
+  const bool reg = k == U && src_chain_reg64();
+  const bool sl = slice64(), nv2 = !reg && fused_nv(sl, k) == 2;
+  if (reg) {
+    if (sl) FUSED64_X0(true, true, 1); else FUSED64_X0(true, false, 1);
+  } else if (sl) {
+    if (nv2) FUSED64_X0(false, true, 2); else FUSED64_X0(false, true, 1);
   } else {
-    if (xr.rows & 1u) FUSED64_LAUNCH(false, true, lds); else FUSED64_LAUNCH(false, false, lds);
+    if (nv2) FUSED64_X0(false, false, 2); else FUSED64_X0(false, false, 1);
   }
+#undef FUSED64_X0
 #undef FUSED64_LAUNCH
 }
 
 template <int P>
 void fused64_pass(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
                   const uint32_t* tbl, int len, int k, unsigned nitems,
-                  const isal_hip_crc64_geom& g, const isal_hip_xrows& xr, const uint64_t* tabs,
-                  uint64_t* part) {
+                  const isal_hip_crc64_geom& g, const isal_hip_xrows& xr, int refl,
+                  const uint64_t* tabs, uint64_t* part) {
   switch (group_u(k)) {
 #define FUSED64_U(u) \
-  case u: launch_fused64<P, u>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, xr, tabs, part); break;
+  case u: launch_fused64<P, u>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, xr, refl, tabs, part); break;
     FUSED64_U(12) FUSED64_U(10) FUSED64_U(8) FUSED64_U(6) FUSED64_U(5)
 #undef FUSED64_U
-    default: launch_fused64<P, 4>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, xr, tabs, part);
+    default: launch_fused64<P, 4>(grid, s, ptrs, ptr_stride, tbl, len, k, nitems, g, xr, refl, tabs, part);
   }
 }
+
+// The fused kernels of one P live in their own object (crc64_fused_pP.o, this
+// file compiled with -DISAL_FUSED64_PART=P): the (P, U, REG, X0, SL) variants
+// of all eight P in one translation unit took the compiler over 20 minutes.
+}  // namespace
+
+#define FUSED64_PART_FN2(p) isal_hip_fused64_part_##p
+#define FUSED64_PART_FN(p) FUSED64_PART_FN2(p)
+extern "C" void FUSED64_PART_FN(ISAL_FUSED64_PART)(
+    unsigned nitems, hipStream_t s, const uint64_t* ptrs, int nsh, const uint32_t* tbl, int len,
+    int k, const isal_hip_crc64_geom* g, const isal_hip_xrows* xr, int refl, const uint64_t* tabs,
+    uint64_t* part) {
+  fused64_pass<ISAL_FUSED64_PART>(nitems, s, ptrs, nsh, tbl, len, k, nitems, *g, *xr, refl, tabs,
+                                  part);
+}
+
+#endif  // ISAL_FUSED64_PART
+
+#ifndef ISAL_FUSED64_PART
 
 int launch_combine64(const uint64_t* part, const uint64_t* ptrs, int ptr_stride, int nsh, int len,
                      const isal_hip_crc64_geom& g, int refl, const uint64_t* tabs,
@@ -594,6 +721,17 @@ int launch_combine64(const uint64_t* part, const uint64_t* ptrs, int ptr_stride,
 }
 
 }  // namespace
+
+// Fused encode+CRC64 launchers, one object per P (crc64_fused_pP.o).
+#define FUSED64_PART_DECL(p)                                                                     \
+  extern "C" void isal_hip_fused64_part_##p(unsigned nitems, hipStream_t s, const uint64_t* ptrs, \
+                                            int nsh, const uint32_t* tbl, int len, int k,       \
+                                            const isal_hip_crc64_geom* g,                       \
+                                            const isal_hip_xrows* xr, int refl,                 \
+                                            const uint64_t* tabs, uint64_t* part);
+FUSED64_PART_DECL(1) FUSED64_PART_DECL(2) FUSED64_PART_DECL(3) FUSED64_PART_DECL(4)
+FUSED64_PART_DECL(5) FUSED64_PART_DECL(6) FUSED64_PART_DECL(7) FUSED64_PART_DECL(8)
+#undef FUSED64_PART_DECL
 
 extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int nsh,
                                      long long nstripes, int len, int vec16, int refl, int tt,
@@ -661,7 +799,7 @@ extern "C" int isal_hip_launch_encode_crc64(const uint64_t* d_ptrs, int k, int r
     uint64_t* part = d_part + static_cast<size_t>(s0) * nsh * g.nblk * kBlock;
     switch (rows) {
 #define FUSED64_P(p) \
-  case p: fused64_pass<p>(nitems, s, ptrs, nsh, d_tbl, len, k, nitems, g, xr, d_tabs, part); break;
+  case p: isal_hip_fused64_part_##p(nitems, s, ptrs, nsh, d_tbl, len, k, &g, &xr, refl, d_tabs, part); break;
       FUSED64_P(1) FUSED64_P(2) FUSED64_P(3) FUSED64_P(4) FUSED64_P(5) FUSED64_P(6) FUSED64_P(7)
       FUSED64_P(8)
 #undef FUSED64_P
@@ -675,3 +813,5 @@ extern "C" int isal_hip_launch_encode_crc64(const uint64_t* d_ptrs, int k, int r
   }
   return 0;
 }
+
+#endif  // !ISAL_FUSED64_PART

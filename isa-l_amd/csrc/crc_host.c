@@ -130,6 +130,26 @@ isal_hip_crc32c_tables(uint32_t *tabs)
                 }
 }
 
+/* Byte-position tables (ISAL_HIP_CRC_B16_TAB): out[p * 256 + b] = crc of byte
+ * b followed by 15 - p zero bytes. */
+void
+isal_hip_crc32c_byte_tables(uint32_t *out)
+{
+        uint32_t slice[ISAL_HIP_CRC_SLICES][256];
+        int s, b;
+        pthread_once(&once, init);
+        for (b = 0; b < 256; b++)
+                slice[0][b] = t0[b];
+        for (s = 1; s < ISAL_HIP_CRC_SLICES; s++)
+                for (b = 0; b < 256; b++) {
+                        const uint32_t c = slice[s - 1][b];
+                        slice[s][b] = (c >> 8) ^ t0[c & 0xff];
+                }
+        for (s = 0; s < ISAL_HIP_CRC_SLICES; s++)
+                for (b = 0; b < 256; b++)
+                        out[s * 256 + b] = slice[ISAL_HIP_CRC_SLICES - 1 - s][b];
+}
+
 /* Tables of the multi-tile chain step from the base tables: every entry of a
  * chunk map shifted by m tiles is entry * x^(8*4096*m) mod P; Z^(4096*4) of a
  * field value is its Z^4096 entry shifted by three more tiles. */

@@ -82,7 +82,7 @@ __device__ __forceinline__ uint32_t chunk_map(const uint32_t* t, uint32_t w0, ui
 }
 
 // crc(0, 16 bytes): 28 conflict-free lookups.
-__device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, uint32_t w0, uint32_t w1,
+__device__ __forceinline__ __attribute__((unused)) uint32_t chunk_crc(const uint32_t* lt, uint32_t w0, uint32_t w1,
                                               uint32_t w2, uint32_t w3) {
   return chunk_map(lt + ISAL_HIP_CRC_CHUNK_TAB, w0, w1, w2, w3);
 }
@@ -96,15 +96,63 @@ __device__ __forceinline__ uint32_t shift_tile(const uint32_t* lt, uint32_t a) {
   return lookup7(lt + ISAL_HIP_CRC_SHIFT_TAB, a);
 }
 
+// ---- byte-indexed chunk path (NB dwords of each chunk) ----------------------
+// The fused kernels are VALU-issue-bound: a 5-bit field lookup
+// costs ~1.6 VALU for its offset. A byte lookup's offset is one SDWA shift
+// (byte select + << 2), so dword d < NB of a chunk goes through the 16
+// position tables of crc(0, chunk) instead (ISAL_HIP_CRC_B16_TAB, table 4d + j
+// = byte j of dword d): 4 lookups instead of 7, traded for LDS bank conflicts
+// (256 entries on 32 banks).
+constexpr int kB16 = kCrcTabDw;  // LDS offset of the byte tables
+
+__device__ __forceinline__ void byte_offs4(uint32_t w, uint32_t (&o)[4]) {
+  const uint32_t two = 2;
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+      : "=v"(o[0]) : "v"(two), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+      : "=v"(o[1]) : "v"(two), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+      : "=v"(o[2]) : "v"(two), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+      : "=v"(o[3]) : "v"(two), "v"(w));
+}
+
+// r ^= the 4 byte lookups of dword d of a chunk.
+__device__ __forceinline__ __attribute__((unused)) uint32_t lookup4b(uint32_t r, const uint32_t* lt, int d, uint32_t w) {
+  uint32_t o[4];
+  byte_offs4(w, o);
+  const char* b = reinterpret_cast<const char*>(lt + kB16 + d * 1024);
+  auto at = [&](int j) { return *reinterpret_cast<const uint32_t*>(b + j * 1024 + o[j]); };
+  return xor3(xor3(r, at(0), at(1)), at(2), at(3));
+}
+
+// crc(0, 16 bytes), dwords d < NB through the byte tables.
+template <int NB>
+__device__ __forceinline__ uint32_t chunk_crc_nb(const uint32_t* lt, uint32_t w0, uint32_t w1,
+                                                 uint32_t w2, uint32_t w3) {
+  if constexpr (NB == 0) {
+    return chunk_crc(lt, w0, w1, w2, w3);
+  } else {
+    constexpr int D = ISAL_HIP_CRC_FIELDS * 32;
+    const uint32_t* t = lt + ISAL_HIP_CRC_CHUNK_TAB;
+    uint32_t r = 0;
+    r = NB > 0 ? lookup4b(r, lt, 0, w0) : r ^ lookup7(t, w0);
+    r = NB > 1 ? lookup4b(r, lt, 1, w1) : r ^ lookup7(t + D, w1);
+    r = NB > 2 ? lookup4b(r, lt, 2, w2) : r ^ lookup7(t + 2 * D, w2);
+    r = NB > 3 ? lookup4b(r, lt, 3, w3) : r ^ lookup7(t + 3 * D, w3);
+    return r;
+  }
+}
+
 // crc(0, nb bytes) one byte at a time (the lane that straddles len).
-__device__ __forceinline__ uint32_t bytes_crc(const uint32_t* lt, const uint8_t* p, int nb) {
+__device__ __forceinline__ __attribute__((unused)) uint32_t bytes_crc(const uint32_t* lt, const uint8_t* p, int nb) {
   uint32_t c = 0;
   for (int i = 0; i < nb; ++i) c = (c >> 8) ^ lt[(c ^ p[i]) & 0xff];
   return c;
 }
 
 // a * b mod P (reflected; bit 31 = x^0), as isal_hip_crc32c_mulmod.
-__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
+__device__ __forceinline__ __attribute__((unused)) uint32_t crc_mulmod(uint32_t a, uint32_t b) {
   uint32_t p = 0;
 #pragma unroll 8
   for (int i = 0; i < 32; ++i) {
@@ -114,6 +162,8 @@ __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
   }
   return p;
 }
+
+#ifndef ISAL_FUSED_PART  // standalone kernels and the combine: the main object only
 
 // ---------------------------------------------------------------------------
 // Standalone: partials of nsh shards per stripe. Item = (stripe, shard, block).
@@ -220,6 +270,58 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards(
 }
 
 // ---------------------------------------------------------------------------
+// Combine: one workgroup per shard (grid-stride). Lane L folds its partials of
+// every block (Horner with the byte tables of x^(8*4096*tt); the last block
+// uses x^(8*4096*nfull_last)), multiplies by W[L] to move them to the shard
+// end, adds its ragged-tile chunk times Ct[L]; the XOR of all lanes plus
+// x^(8*len) * init is crc32_iscsi(shard, len, init).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void crc32c_combine(
+    const uint32_t* __restrict__ part, const uint32_t* __restrict__ tail,
+    const uint32_t* __restrict__ plan, unsigned nblk, int has_tail, unsigned init,
+    uint32_t* __restrict__ out, unsigned nsh) {
+  __shared__ uint32_t kt[2048];
+  __shared__ uint32_t red[kBlock / 64];
+  for (int i = threadIdx.x; i < 2048; i += kBlock) kt[i] = plan[i];
+  __syncthreads();
+  const uint32_t wl = plan[2048 + threadIdx.x];
+  const uint32_t cl = plan[2304 + threadIdx.x];
+  const uint32_t xlen = plan[2560];
+  for (unsigned sh = blockIdx.x; sh < nsh; sh += gridDim.x) {
+    const uint32_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + threadIdx.x;
+    uint32_t h = 0;
+    for (unsigned b = 0; b < nblk; ++b) {
+      const uint32_t* k4 = (b + 1 == nblk) ? kt + 1024 : kt;
+      h = xor3(k4[h & 0xff], k4[256 + ((h >> 8) & 0xff)], k4[512 + ((h >> 16) & 0xff)]) ^
+          k4[768 + (h >> 24)] ^ pp[static_cast<size_t>(b) * kBlock];
+    }
+    uint32_t v = crc_mulmod(h, wl);
+    if (has_tail) v ^= crc_mulmod(tail[static_cast<size_t>(sh) * kBlock + threadIdx.x], cl);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) out[sh] = red[0] ^ red[1] ^ red[2] ^ red[3] ^ crc_mulmod(init, xlen);
+    __syncthreads();
+  }
+}
+
+constexpr unsigned kMaxCrcItems = 1u << 30;
+
+// Tiles per chain step of crc32c_shards (ISAL_HIP_CRC_STEP = 1 or 4). Unlike
+// CRC64 the CRC32C kernel is not bound by its lookups: step 4 measured 2.90 ms
+// vs 2.87 ms per C2 step (profiles/r01_crc_step_sweep.txt), so 1 by default.
+int crc_step() {
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC_STEP) == 4 ? 4 : 1;
+}
+
+unsigned crc_grid(unsigned long long nitems) {
+  return static_cast<unsigned>(nitems);
+}
+
+#else  // ISAL_FUSED_PART: the fused kernels of one P (crc_fused_pP.o)
+
+// ---------------------------------------------------------------------------
 // Fused encode + CRC. The encode half is ec_encode_v16's (same loads, same
 // GF arithmetic, same stores); the source chunks already in registers and the
 // parity chunks about to be stored also feed the CRC chains. Output chains
@@ -235,7 +337,7 @@ enum : int {
   kFeedNone = 3,  // no source checksums (second pass of rows > 8)
 };
 
-template <int FEED>
+template <int FEED, int NB = 0>
 struct SrcFeed {
   const uint32_t* lt;
   uint32_t* la;    // [k][256] source chains (LDS)
@@ -243,7 +345,7 @@ struct SrcFeed {
   uint32_t* tail;  // tail row of source shard 0 of this stripe
   __device__ __forceinline__ void operator()(int j, const uint4& x) const {
     if constexpr (FEED != kFeedNone) {
-      const uint32_t c = chunk_crc(lt, x);
+      const uint32_t c = chunk_crc_nb<NB>(lt, x.x, x.y, x.z, x.w);
       if constexpr (FEED == kFeedReg) {
         ra[j] = shift_tile(lt, ra[j]) ^ c;
       } else if constexpr (FEED == kFeedLds) {
@@ -333,7 +435,8 @@ constexpr int crc_waves() {
 // from those sources' chains instead of per tile. (A compile-time choice: a
 // runtime row mask inside the tile loop costs the register-tight kernel its
 // registers.)
-template <int P, class Pol, bool REG, bool SRC, bool X0 = false>
+// NB: dwords of each chunk through the byte tables (chunk_crc_nb).
+template <int P, class Pol, bool REG, bool SRC, bool X0 = false, int NB = 0>
 __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_encode_crc_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned nblk, unsigned tt,
@@ -343,9 +446,11 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
   constexpr int kFull = SRC ? (REG ? kFeedReg : kFeedLds) : kFeedNone;
   constexpr int kRag = SRC ? kFeedTail : kFeedNone;
   constexpr int NR = REG ? Pol::U : 1;
-  __shared__ uint32_t lt[kCrcTabDw];
+  __shared__ uint32_t lt[kCrcTabDw + NB * 1024];
   extern __shared__ uint32_t la[];  // [k][kBlock] when SRC && !REG
-  load_crc_tables(lt, tabs);
+  if constexpr (NB > 0)
+    for (int i = threadIdx.x; i < NB * 1024; i += kBlock) lt[kB16 + i] = tabs[ISAL_HIP_CRC_B16_TAB + i];
+  load_crc_tables(lt, tabs);  // (its barrier covers the byte tables too)
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned stripe = w / nblk, blk = w - stripe * nblk;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
@@ -377,13 +482,13 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
         for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
         int z = 0;  // opaque zero: see below
         asm volatile("" : "+s"(z));
-        mac_feed16<P, Pol::U>(acc, x, 0, tbl + z, SrcFeed<kFull>{lt, la, ra, tail + shard_s * kBlock});
+        mac_feed16<P, Pol::U>(acc, x, 0, tbl + z, SrcFeed<kFull, NB>{lt, la, ra, tail + shard_s * kBlock});
 #pragma unroll
         for (int l = 0; l < P; ++l) {
           store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
                            len);
           if (!(X0 && l == 0))
-            ao[l] = shift_tile(lt, ao[l]) ^ chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+            ao[l] = shift_tile(lt, ao[l]) ^ chunk_crc_nb<NB>(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
         }
       }
     } else {
@@ -395,13 +500,13 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
         int z = 0;
         asm volatile("" : "+s"(z));
         accum16_crc<P, Pol, REG>(acc, sp + src0, tbl + z, k, off, len,
-                                 SrcFeed<kFull>{lt, la, ra, tail + shard_s * kBlock});
+                                 SrcFeed<kFull, NB>{lt, la, ra, tail + shard_s * kBlock});
 #pragma unroll
         for (int l = 0; l < P; ++l) {
           store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
                            len);
           if (!(X0 && l == 0))
-            ao[l] = shift_tile(lt, ao[l]) ^ chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+            ao[l] = shift_tile(lt, ao[l]) ^ chunk_crc_nb<NB>(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
         }
       }
     }
@@ -459,61 +564,11 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
   }
 }
 
-// ---------------------------------------------------------------------------
-// Combine: one workgroup per shard (grid-stride). Lane L folds its partials of
-// every block (Horner with the byte tables of x^(8*4096*tt); the last block
-// uses x^(8*4096*nfull_last)), multiplies by W[L] to move them to the shard
-// end, adds its ragged-tile chunk times Ct[L]; the XOR of all lanes plus
-// x^(8*len) * init is crc32_iscsi(shard, len, init).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void crc32c_combine(
-    const uint32_t* __restrict__ part, const uint32_t* __restrict__ tail,
-    const uint32_t* __restrict__ plan, unsigned nblk, int has_tail, unsigned init,
-    uint32_t* __restrict__ out, unsigned nsh) {
-  __shared__ uint32_t kt[2048];
-  __shared__ uint32_t red[kBlock / 64];
-  for (int i = threadIdx.x; i < 2048; i += kBlock) kt[i] = plan[i];
-  __syncthreads();
-  const uint32_t wl = plan[2048 + threadIdx.x];
-  const uint32_t cl = plan[2304 + threadIdx.x];
-  const uint32_t xlen = plan[2560];
-  for (unsigned sh = blockIdx.x; sh < nsh; sh += gridDim.x) {
-    const uint32_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + threadIdx.x;
-    uint32_t h = 0;
-    for (unsigned b = 0; b < nblk; ++b) {
-      const uint32_t* k4 = (b + 1 == nblk) ? kt + 1024 : kt;
-      h = xor3(k4[h & 0xff], k4[256 + ((h >> 8) & 0xff)], k4[512 + ((h >> 16) & 0xff)]) ^
-          k4[768 + (h >> 24)] ^ pp[static_cast<size_t>(b) * kBlock];
-    }
-    uint32_t v = crc_mulmod(h, wl);
-    if (has_tail) v ^= crc_mulmod(tail[static_cast<size_t>(sh) * kBlock + threadIdx.x], cl);
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) out[sh] = red[0] ^ red[1] ^ red[2] ^ red[3] ^ crc_mulmod(init, xlen);
-    __syncthreads();
-  }
-}
-
-constexpr unsigned kMaxCrcItems = 1u << 30;
-
 // Memory policy of the fused kernel: non-temporal global loads/stores (a
 // 64-bit SGPR base per shard instead of a 4-SGPR buffer descriptor: the CRC
 // half needs the scalar registers).
 template <int UU>
 using FusedPol = EncPol<UU, kNT, kNT>;
-
-// Tiles per chain step of crc32c_shards (ISAL_HIP_CRC_STEP = 1 or 4). Unlike
-// CRC64 the CRC32C kernel is not bound by its lookups: step 4 measured 2.90 ms
-// vs 2.87 ms per C2 step (profiles/r01_crc_step_sweep.txt), so 1 by default.
-int crc_step() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC_STEP) == 4 ? 4 : 1;
-}
-
-unsigned crc_grid(unsigned long long nitems) {
-  return static_cast<unsigned>(nitems);
-}
 
 int enc_group_crc(int k) {
   static const int cand[] = {12, 10, 8, 6, 5, 4};
@@ -531,26 +586,37 @@ bool src_chain_reg() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC_SRC_CHAIN) == 1;  // "reg"
 }
 
+// Dwords per chunk through the byte tables in the fused kernel with LDS
+// source chains: all four by default (ISAL_HIP_CRC_BYTE_DWORDS=0 selects the
+// field tables). C2 step 3.74 -> 3.48 ms (VALU 2.11e9 -> 1.65e9
+// wave-instructions; the LDS array is then ~76 % busy, half of it bank
+// conflicts: profiles/r02_fastcrc_*).
+int crc_byte_dwords() {
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC_BYTE_DWORDS) == 0 ? 0 : 4;
+}
+
 template <int P, int U>
 void launch_fused(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
                   int src0, int dst0, const uint32_t* tbl, int len, int k, unsigned nitems,
                   const isal_hip_crc_geom& g, const isal_hip_xrows& xr, const uint32_t* tabs,
                   uint32_t* part, uint32_t* tail, int nshard_total, int crc_src, int out_shard0) {
-#define FUSED_LAUNCH(REG, SRC, X0, LDS)                                                          \
-  hipLaunchKernelGGL((ec_encode_crc_v16<P, FusedPol<U>, REG, SRC, X0>), dim3(grid), dim3(kBlock),  \
+#define FUSED_LAUNCH(REG, SRC, X0, LDS, NB)                                                      \
+  hipLaunchKernelGGL((ec_encode_crc_v16<P, FusedPol<U>, REG, SRC, X0, NB>), dim3(grid), dim3(kBlock), \
                      LDS, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems,                    \
                      static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),                   \
                      static_cast<unsigned>(g.nfull), static_cast<unsigned>(g.ntiles), xr.src[0],  \
                      tabs, part, tail, nshard_total, out_shard0)
   const bool x0 = crc_src && (xr.rows & 1u);
+  const bool nb4 = crc_byte_dwords() == 4;
   if (!crc_src)
-    FUSED_LAUNCH(false, false, false, 0);
+    FUSED_LAUNCH(false, false, false, 0, 0);
   else if (k == U && src_chain_reg())  // one load group: source chains in registers (no X0:
-    FUSED_LAUNCH(true, true, false, 0);  // its 2 extra SGPRs make the register variant spill)
-  else if (x0)
-    FUSED_LAUNCH(false, true, true, lds);
-  else
-    FUSED_LAUNCH(false, true, false, lds);
+    FUSED_LAUNCH(true, true, false, 0, 0);  // its 2 extra SGPRs make the register variant spill)
+  else if (x0) {
+    if (nb4) FUSED_LAUNCH(false, true, true, lds, 4); else FUSED_LAUNCH(false, true, true, lds, 0);
+  } else {
+    if (nb4) FUSED_LAUNCH(false, true, false, lds, 4); else FUSED_LAUNCH(false, true, false, lds, 0);
+  }
 #undef FUSED_LAUNCH
 }
 
@@ -574,6 +640,34 @@ void fused_pass(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs, 
 }
 
 }  // namespace
+
+// The fused kernels of one P live in their own object (this file compiled with
+// -DISAL_FUSED_PART=P) so the variants build in parallel.
+#define FUSED_PART_FN2(p) isal_hip_fused_crc_part_##p
+#define FUSED_PART_FN(p) FUSED_PART_FN2(p)
+extern "C" void FUSED_PART_FN(ISAL_FUSED_PART)(
+    unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
+    const uint32_t* tbl, int len, int k, unsigned nitems, const isal_hip_crc_geom* g,
+    const isal_hip_xrows* xr, const uint32_t* tabs, uint32_t* part, uint32_t* tail, int nshard_total,
+    int crc_src, int out_shard0) {
+  fused_pass<ISAL_FUSED_PART>(grid, lds, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, *g, *xr,
+                              tabs, part, tail, nshard_total, crc_src, out_shard0);
+}
+#endif  // ISAL_FUSED_PART
+
+#ifndef ISAL_FUSED_PART
+}  // namespace
+
+// Fused encode+CRC32C launchers, one object per P (crc_fused_pP.o).
+#define FUSED_PART_DECL(p)                                                                          \
+  extern "C" void isal_hip_fused_crc_part_##p(                                                      \
+      unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,     \
+      int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, const isal_hip_crc_geom* g,   \
+      const isal_hip_xrows* xr, const uint32_t* tabs, uint32_t* part, uint32_t* tail,               \
+      int nshard_total, int crc_src, int out_shard0);
+FUSED_PART_DECL(1) FUSED_PART_DECL(2) FUSED_PART_DECL(3) FUSED_PART_DECL(4)
+FUSED_PART_DECL(5) FUSED_PART_DECL(6) FUSED_PART_DECL(7) FUSED_PART_DECL(8)
+#undef FUSED_PART_DECL
 
 extern "C" int isal_hip_launch_crc(const uint64_t* d_ptrs, int ptr_stride, int idx0, int nsh,
                                    long long nstripes, int len, int vec16, int tt,
@@ -640,8 +734,9 @@ extern "C" int isal_hip_launch_encode_crc(const uint64_t* d_ptrs, int ptr_stride
       switch (P) {
 #define FUSED_CASE(n)                                                                          \
   case n:                                                                                      \
-    fused_pass<n>(crc_grid(nitems), lds, s, ptrs, ptr_stride, src_idx0, dst_idx0 + r0, tbl, len, \
-                  k, nitems, g, xr, d_tabs, part, tail, nshard_total, crc_src, k + r0);        \
+    isal_hip_fused_crc_part_##n(crc_grid(nitems), lds, s, ptrs, ptr_stride, src_idx0,          \
+                                dst_idx0 + r0, tbl, len, k, nitems, &g, &xr, d_tabs, part,     \
+                                tail, nshard_total, crc_src, k + r0);                          \
     break;
         FUSED_CASE(1) FUSED_CASE(2) FUSED_CASE(3) FUSED_CASE(4) FUSED_CASE(5) FUSED_CASE(6)
         FUSED_CASE(7) FUSED_CASE(8)
@@ -667,3 +762,5 @@ extern "C" int isal_hip_launch_crc_combine(const uint32_t* d_part, const uint32_
   isal_hip_count_launch();
   return static_cast<int>(hipGetLastError());
 }
+
+#endif  // !ISAL_FUSED_PART

@@ -680,6 +680,33 @@ def test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, chain, xro
     b.close()
 
 
+@pytest.mark.parametrize("nb", ["4", "0"])
+@pytest.mark.parametrize("k,rows,n,ns,skew", CRC_SHAPES)
+def test_encode_crc_byte_tables(engine, oracle, gpu, monkeypatch, nb, k, rows, n, ns, skew):
+    """The fused CRC32C kernel with every chunk dword through the byte-position
+    tables (ISAL_HIP_CRC_BYTE_DWORDS=4, the default) and through the 5-bit
+    field tables (=0) == oracle."""
+    _setenv(monkeypatch, "ISAL_HIP_CRC_BYTE_DWORDS", nb)
+    test_encode_crc_vs_oracle(engine, oracle, gpu, k, rows, n, ns, skew)
+
+
+@pytest.mark.parametrize("tt", [1, 3, 16])
+def test_encode_crc_field_tables_tiles(engine, oracle, gpu, monkeypatch, tt):
+    _setenv(monkeypatch, "ISAL_HIP_CRC_BYTE_DWORDS", "0")
+    test_encode_crc_tiles_per_workgroup(engine, oracle, gpu, monkeypatch, 7, 3, tt)
+
+
+@pytest.mark.parametrize("xrows", ["1", "0"])
+@pytest.mark.parametrize("k,n,tt", [(10, 4096 * 37 + 2048, 4), (7, 65536, None)])
+def test_fused_crc_derived_xor_rows_fast_paths(engine, oracle, gpu, monkeypatch, xrows, k, n, tt):
+    """Derived XOR rows with the byte-table CRC32C path and the slicing CRC64
+    path (two lane groups per workgroup)."""
+    _setenv(monkeypatch, "ISAL_HIP_CRC_BYTE_DWORDS", "4")
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", "1")
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_NV", "2")
+    test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, "lds", xrows, k, n, tt)
+
+
 def test_encode_crc_c2_full_size(engine, oracle, gpu):
     """C2 at full size through the fused path: parity identical to the plain
     encode kernel's, CRCs == oracle on sampled stripes and == the standalone
@@ -837,6 +864,35 @@ def test_encode_crc64_knobs(engine, oracle, gpu, monkeypatch, pair, chain, k, ro
     _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_PAIR", str(pair))
     _setenv(monkeypatch, "ISAL_HIP_CRC64_SRC_CHAIN", chain)
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant)
+
+
+@pytest.mark.parametrize("slice_,pair,chain,nv", [
+    ("1", 1, "lds", 1), ("1", 0, "lds", 1), ("1", 1, "reg", 1), ("1", 0, "reg", 1),
+    ("1", 1, "lds", 2), ("1", 0, "lds", 2), ("0", 1, "lds", 2), ("0", 0, "lds", 2),
+    ("0", 1, "lds", 1), ("0", 1, "reg", 1)])
+@pytest.mark.parametrize("k,rows,n,ns,skew,tt,variant", ENCODE_CRC64_SHAPES[:5])
+def test_encode_crc64_slice_knobs(engine, oracle, gpu, monkeypatch, slice_, pair, chain, nv, k, rows, n,
+                                  ns, skew, tt, variant):
+    """The slicing-by-8 chunk path of the fused kernel (ISAL_HIP_CRC64_SLICE=1,
+    u-domain chains) and two 256-lane groups per workgroup
+    (ISAL_HIP_CRC64_FUSED_NV=2) == oracle, paired and unpaired steps, both
+    chain homes."""
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", slice_)
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_NV", str(nv))
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_PAIR", str(pair))
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_SRC_CHAIN", chain)
+    test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant)
+
+
+@pytest.mark.parametrize("slice_", ["0", "1"])
+@pytest.mark.parametrize("variant", range(8))
+def test_encode_crc64_every_flavour(engine, oracle, gpu, monkeypatch, variant, slice_):
+    """All eight crc64.h flavours through the fused kernel, field-table and
+    slicing paths (the slicing path byte-swaps the norm flavours' chains)."""
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", slice_)
+    test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 10, 4, 4096 * 37 + 2048, 3, 0, 4,
+                                variant)
+    test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 7, 3, 4096 * 20, 2, 0, 3, variant)
 
 
 def test_encode_crc64_c2_full_size(engine, oracle, gpu):

@@ -72,6 +72,41 @@ for s in $STEPS; do
                 run pmc_write_crc64 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_crc64" -o w -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 3 --warmup 1
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_crc64.csv" "workload=crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_crc64" "$OUT/pmc_write_crc64" crc64_shards
                 ;;
+        slice64)
+                # fused encode+CRC64: field tables vs slicing-by-8 chunk path, 1 or 2 lane groups per workgroup
+                run pytest_gpu_encrc64 500 python -u -m pytest tests -m gpu -x -v -k "encode_crc64" --timeout 200 --timeout-method thread
+                for cfg in ${SLICE64_CFGS:-0:1 0:2 1:1 1:2}; do
+                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run bench_encrc64_sl${cfg/:/_nv} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
+                done
+                for cfg in ${SLICE64_PMC:-1:2 0:2}; do
+                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run pmc_lds_sl${cfg/:/_nv} 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_sl${cfg/:/_nv}" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
+                done
+                ;;
+        fastcrc)
+                # byte-indexed CRC paths of the fused kernels: CRC32C byte tables, CRC64 slicing (+ lane groups)
+                run pytest_gpu_crc 700 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
+                for nb in 0 4; do
+                        ISAL_HIP_CRC_BYTE_DWORDS=$nb run bench_encrc_nb$nb 300 python bench.py --workload encode-crc --no-cpu-baseline
+                done
+                for cfg in ${SLICE64_CFGS:-0:1 0:2 1:1 1:2}; do
+                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run bench_encrc64_sl${cfg/:/_nv} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
+                done
+                ISAL_HIP_CRC_BYTE_DWORDS=4 run pmc_lds_encrc_nb4 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_encrc_nb4" -o l -- python3 bench.py --workload encode-crc --no-cpu-baseline --steps 2 --warmup 1
+                for cfg in ${SLICE64_PMC:-1:2 0:2}; do
+                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run pmc_lds_sl${cfg/:/_nv} 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_sl${cfg/:/_nv}" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
+                done
+                ;;
+        crcp)
+                # fast CRC paths vs field tables at fewer parity rows (less encode VALU to hide behind)
+                for p in 1 2; do
+                        for nb in 0 4; do
+                                ISAL_HIP_CRC_BYTE_DWORDS=$nb run bench_encrc_p${p}_nb$nb 300 python bench.py --workload encode-crc --p $p --no-cpu-baseline
+                        done
+                        for sl in 0 1; do
+                                ISAL_HIP_CRC64_SLICE=$sl run bench_encrc64_p${p}_sl$sl 300 python bench.py --workload encode-crc64 --p $p --no-cpu-baseline
+                        done
+                done
+                ;;
         encrc64sweep)
                 for cfg in ${ENCRC64_CFGS:-reg:10 lds:10 lds:5}; do
                         ISAL_HIP_CRC64_SRC_CHAIN=${cfg%:*} ISAL_HIP_CRC64_FUSED_U=${cfg#*:} run bench_encrc64_${cfg/:/_u} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
