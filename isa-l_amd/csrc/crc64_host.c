@@ -177,11 +177,12 @@ pi_of(int variant, uint64_t x)
 static void
 slice_tables(int variant, uint64_t *tabs)
 {
-        uint64_t z[64], zu[64];
+        uint64_t z[64];
         uint8_t d[8];
-        int j, v, i, s;
+        int j, v;
         uint64_t *a = tabs + ISAL_HIP_CRC64_SLICE_TAB, *b = a + 8 * 256;
-        isal_hip_crc64_zpow(variant, ISAL_HIP_CRC_TILE, z);
+        /* A' = Z^4080_u o A: the pre-shifted chain's step (crc64_kernels.hip) */
+        isal_hip_crc64_zpow(variant, ISAL_HIP_CRC_TILE - 16, z);
         for (j = 0; j < 8; j++)
                 for (v = 0; v < 256; v++) {
                         uint64_t r;
@@ -191,13 +192,6 @@ slice_tables(int variant, uint64_t *tabs)
                         a[j * 256 + v] = pi_of(variant, r);
                         b[j * 256 + v] = pi_of(variant, apply(z, r));
                 }
-        /* pi Z^(4096 s) pi as field tables, s = 1, 2 */
-        for (s = 1; s <= 2; s++) {
-                isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * s, z);
-                for (i = 0; i < 64; i++)
-                        zu[i] = pi_of(variant, apply(z, pi_of(variant, 1ULL << i)));
-                op_tables(zu, tabs + ISAL_HIP_CRC64_UOP_TAB + (s - 1) * ISAL_HIP_CRC64_OP_ENTRIES);
-        }
 }
 
 /* Layout: isal_hip_internal.h (ISAL_HIP_CRC64_*). */

@@ -368,15 +368,21 @@ __device__ __forceinline__ uint64_t chain_step(const uint64_t* lt, uint64_t a, u
 
 // ---- slicing-by-8 chunk path of the fused kernel (SL) ----------------------
 // The field-table path costs ~1.7 VALU per 5-bit field offset + 1 per 64-bit
-// fold, 28 lookups per 16-byte chunk, and the fused kernel is VALU-issue-bound
-// (DESIGN §3). Here a chunk is two slicing-by-8 steps in the u-domain
-// (crc64_host.c: u = pi(s), one update rule for every flavour):
-//   u1 = A(lo8),  raw_u(chunk) = A(hi8 ^ u1),  T1_u(chunk) = B(hi8 ^ u1)
-// 16 byte-indexed lookups, each offset one SDWA shift (byte select + << 3).
-// The 256-entry tables are not bank-conflict-free (8 entries per bank pair):
-// this trades VALU issue for LDS cycles.
-constexpr int kSA = 0, kSB = 8 * 256, kSZ1 = 16 * 256, kSZ2 = kSZ1 + kOp;
-constexpr int kSlLds = kSZ2 + kOp;
+// fold, 28 lookups per 16-byte chunk plus 7 per tile for the chain step, and
+// the fused kernel is VALU-issue-bound. Here, in the u-domain
+// (crc64_host.c: u = pi(s), one update rule u' = A(d ^ u) for every flavour),
+// a lane keeps its chain PRE-SHIFTED: b = Z^4080_u(a), the chain advanced by
+// the 4080 bytes of the other lanes' chunks that follow its own in the tile.
+// Then the next tile's raw value is raw_u(b, chunk) — b is XORed into the
+// chunk's first 8 bytes like a CRC register — and the step needs no separate
+// shift map at all:
+//   u1 = A(lo8 ^ b),  b' = A'(hi8 ^ u1)   (A' = Z^4080_u o A)
+// and the block's last tile ends with A instead of A', leaving the plain
+// chain a. 16 byte-indexed lookups per chunk, each offset one SDWA shift
+// (byte select + << 3); the 256-entry tables are not bank-conflict-free (8
+// entries per bank pair): VALU issue traded for LDS cycles.
+constexpr int kSA = 0, kSB = 8 * 256;  // A, A' in LDS
+constexpr int kSlLds = 16 * 256;
 
 // Byte b of w times 8 (an 8-byte entry's offset) in one VALU op.
 __device__ __forceinline__ void byte_offs8(uint32_t w, uint32_t (&o)[4]) {
@@ -406,15 +412,15 @@ __device__ __forceinline__ void slice8_acc(X64& acc, const uint64_t* t, uint32_t
   acc.add2(tab8_at(t, 6, q[2]), tab8_at(t, 7, q[3]));
 }
 
-// chain_step in the u-domain through the slicing tables.
+// One tile of a pre-shifted u-domain chain b (phase 1: the block's last tile,
+// which returns the plain chain a instead).
 template <int PH>
-__device__ __forceinline__ uint64_t chain_step_sl(const uint64_t* lt, uint64_t a, uint32_t w0,
+__device__ __forceinline__ uint64_t chain_step_sl(const uint64_t* lt, uint64_t b, uint32_t w0,
                                                   uint32_t w1, uint32_t w2, uint32_t w3) {
   X64 u{0u, 0u};
-  slice8_acc(u, lt + kSA, w0, w1);
-  X64 c = PH == 2 ? x64(a) : X64{0u, 0u};
-  if constexpr (PH != 2) apply_op_acc(c, lt + (PH == 1 ? kSZ2 : kSZ1), a);
-  slice8_acc(c, lt + (PH == 1 ? kSB : kSA), w2 ^ u.lo, w3 ^ u.hi);
+  slice8_acc(u, lt + kSA, w0 ^ static_cast<uint32_t>(b), w1 ^ static_cast<uint32_t>(b >> 32));
+  X64 c{0u, 0u};
+  slice8_acc(c, lt + (PH == 1 ? kSA : kSB), w2 ^ u.lo, w3 ^ u.hi);
   return c.get();
 }
 
@@ -444,7 +450,7 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
   __shared__ uint64_t lt[SL ? kSlLds : kKernTab + kCE + kOp];
   extern __shared__ uint64_t la[];  // [k][kBlock * NV] source chains when !REG
   if constexpr (SL) {
-    load_lds<kSlLds, NV>(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB);  // SLICE and UOP are contiguous
+    load_lds<kSlLds, NV>(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB);
   } else {
     load_lds<kKernTab, NV>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
     load_lds<kCE, NV>(lt + kT1, tabs + ISAL_HIP_CRC64_CHUNKX_TAB);
@@ -481,8 +487,12 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
     // applies a = Z^8192(a) ^ T1(chunk), the odd one a ^= raw(0, chunk) — 70
     // lookups per two tiles instead of 84, no extra state; an unpaired tile
     // takes the single step a = Z^4096(a) ^ raw(0, chunk).
+    // SL: phase 1 marks the block's last tile (it returns the plain chain).
     auto phase_of = [&](unsigned t) __attribute__((always_inline)) {
-      return !pair ? 0 : ((t - t0) & 1) ? 2 : (t + 1 < t1 ? 1 : 0);
+      if constexpr (SL)
+        return t + 1 == t1 ? 1 : 0;
+      else
+        return !pair ? 0 : ((t - t0) & 1) ? 2 : (t + 1 < t1 ? 1 : 0);
     };
     auto with_phase = [&](int ph, auto&& body) __attribute__((always_inline)) {
       if (ph == 1)

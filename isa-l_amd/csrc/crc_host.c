@@ -131,11 +131,12 @@ isal_hip_crc32c_tables(uint32_t *tabs)
 }
 
 /* Byte-position tables (ISAL_HIP_CRC_B16_TAB): out[p * 256 + b] = crc of byte
- * b followed by 15 - p zero bytes. */
+ * b followed by 15 - p zero bytes, then the same shifted by 4080 more zero
+ * bytes (multiplied by x^(8*4080) mod P, as the chain shift tables are). */
 void
 isal_hip_crc32c_byte_tables(uint32_t *out)
 {
-        uint32_t slice[ISAL_HIP_CRC_SLICES][256];
+        uint32_t slice[ISAL_HIP_CRC_SLICES][256], zk;
         int s, b;
         pthread_once(&once, init);
         for (b = 0; b < 256; b++)
@@ -145,9 +146,13 @@ isal_hip_crc32c_byte_tables(uint32_t *out)
                         const uint32_t c = slice[s - 1][b];
                         slice[s][b] = (c >> 8) ^ t0[c & 0xff];
                 }
+        zk = isal_hip_crc32c_xpow8n(ISAL_HIP_CRC_TILE - ISAL_HIP_CRC_SLICES);
         for (s = 0; s < ISAL_HIP_CRC_SLICES; s++)
-                for (b = 0; b < 256; b++)
-                        out[s * 256 + b] = slice[ISAL_HIP_CRC_SLICES - 1 - s][b];
+                for (b = 0; b < 256; b++) {
+                        const uint32_t c = slice[ISAL_HIP_CRC_SLICES - 1 - s][b];
+                        out[s * 256 + b] = c;
+                        out[ISAL_HIP_CRC_SLICES * 256 + s * 256 + b] = isal_hip_crc32c_mulmod(c, zk);
+                }
 }
 
 /* Tables of the multi-tile chain step from the base tables: every entry of a

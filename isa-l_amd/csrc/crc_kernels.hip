@@ -22,6 +22,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "ec_device.h"
 
 namespace {
@@ -96,14 +98,20 @@ __device__ __forceinline__ uint32_t shift_tile(const uint32_t* lt, uint32_t a) {
   return lookup7(lt + ISAL_HIP_CRC_SHIFT_TAB, a);
 }
 
-// ---- byte-indexed chunk path (NB dwords of each chunk) ----------------------
+// ---- byte-indexed path with pre-shifted chains (NB = 4) --------------------
 // The fused kernels are VALU-issue-bound: a 5-bit field lookup
-// costs ~1.6 VALU for its offset. A byte lookup's offset is one SDWA shift
-// (byte select + << 2), so dword d < NB of a chunk goes through the 16
-// position tables of crc(0, chunk) instead (ISAL_HIP_CRC_B16_TAB, table 4d + j
-// = byte j of dword d): 4 lookups instead of 7, traded for LDS bank conflicts
-// (256 entries on 32 banks).
-constexpr int kB16 = kCrcTabDw;  // LDS offset of the byte tables
+// costs ~1.6 VALU for its offset, and every tile also pays a 7-lookup Z^4096
+// chain step. Here a lane keeps its chain PRE-SHIFTED, b = Z^4080(a): the
+// chain advanced past the 4080 bytes of the other lanes' chunks that follow
+// its own in the tile. The next tile's raw CRC is then crc(b, chunk) — b is
+// XORed into the chunk's first dword like a CRC register — so a step is one
+// map of the 16 chunk bytes, through byte-position tables:
+//   b' = P'(w0 ^ b, w1, w2, w3)   P' = Z^4080 o P   (P: crc(0, chunk) per byte)
+// and the block's last tile applies P instead, leaving the plain chain a.
+// 16 byte lookups per chunk, each offset one SDWA shift (byte select + << 2),
+// no chain step; the 256-entry tables are not bank-conflict-free (8 entries
+// per bank): VALU issue traded for LDS cycles. LDS: P at 0, P' at 4096 dwords.
+constexpr int kPos = 0, kPosZ = 16 * 256, kPosLds = 32 * 256;
 
 __device__ __forceinline__ void byte_offs4(uint32_t w, uint32_t (&o)[4]) {
   const uint32_t two = 2;
@@ -117,31 +125,27 @@ __device__ __forceinline__ void byte_offs4(uint32_t w, uint32_t (&o)[4]) {
       : "=v"(o[3]) : "v"(two), "v"(w));
 }
 
-// r ^= the 4 byte lookups of dword d of a chunk.
-__device__ __forceinline__ __attribute__((unused)) uint32_t lookup4b(uint32_t r, const uint32_t* lt, int d, uint32_t w) {
+// r ^= the 4 byte lookups of dword d of a chunk in the position tables at t.
+__device__ __forceinline__ __attribute__((unused)) uint32_t lookup4b(uint32_t r, const uint32_t* t,
+                                                                    int d, uint32_t w) {
   uint32_t o[4];
   byte_offs4(w, o);
-  const char* b = reinterpret_cast<const char*>(lt + kB16 + d * 1024);
+  const char* b = reinterpret_cast<const char*>(t + d * 1024);
   auto at = [&](int j) { return *reinterpret_cast<const uint32_t*>(b + j * 1024 + o[j]); };
   return xor3(xor3(r, at(0), at(1)), at(2), at(3));
 }
 
-// crc(0, 16 bytes), dwords d < NB through the byte tables.
-template <int NB>
-__device__ __forceinline__ uint32_t chunk_crc_nb(const uint32_t* lt, uint32_t w0, uint32_t w1,
-                                                 uint32_t w2, uint32_t w3) {
-  if constexpr (NB == 0) {
-    return chunk_crc(lt, w0, w1, w2, w3);
-  } else {
-    constexpr int D = ISAL_HIP_CRC_FIELDS * 32;
-    const uint32_t* t = lt + ISAL_HIP_CRC_CHUNK_TAB;
-    uint32_t r = 0;
-    r = NB > 0 ? lookup4b(r, lt, 0, w0) : r ^ lookup7(t, w0);
-    r = NB > 1 ? lookup4b(r, lt, 1, w1) : r ^ lookup7(t + D, w1);
-    r = NB > 2 ? lookup4b(r, lt, 2, w2) : r ^ lookup7(t + 2 * D, w2);
-    r = NB > 3 ? lookup4b(r, lt, 3, w3) : r ^ lookup7(t + 3 * D, w3);
-    return r;
-  }
+// One tile of a pre-shifted chain b (LAST: the block's last tile, which
+// returns the plain chain; b = 0 gives crc(0, chunk)).
+template <bool LAST>
+__device__ __forceinline__ __attribute__((unused)) uint32_t pre_step(const uint32_t* lt, uint32_t b,
+                                                                    uint32_t w0, uint32_t w1,
+                                                                    uint32_t w2, uint32_t w3) {
+  const uint32_t* t = lt + (LAST ? kPos : kPosZ);
+  uint32_t r = lookup4b(0u, t, 0, w0 ^ b);
+  r = lookup4b(r, t, 1, w1);
+  r = lookup4b(r, t, 2, w2);
+  return lookup4b(r, t, 3, w3);
 }
 
 // crc(0, nb bytes) one byte at a time (the lane that straddles len).
@@ -337,22 +341,36 @@ enum : int {
   kFeedNone = 3,  // no source checksums (second pass of rows > 8)
 };
 
-template <int FEED, int NB = 0>
+// NB = 4: pre-shifted chains (pre_step), LAST marking the block's last tile.
+template <int FEED, int NB = 0, bool LAST = false>
 struct SrcFeed {
   const uint32_t* lt;
-  uint32_t* la;    // [k][256] source chains (LDS)
+  uint32_t* la;    // [k][kBlock * NV] source chains (LDS)
   uint32_t* ra;    // [U] source chains (registers)
   uint32_t* tail;  // tail row of source shard 0 of this stripe
+  unsigned las;    // row stride of la
+  unsigned tid;    // lane within its 256-lane group
   __device__ __forceinline__ void operator()(int j, const uint4& x) const {
     if constexpr (FEED != kFeedNone) {
-      const uint32_t c = chunk_crc_nb<NB>(lt, x.x, x.y, x.z, x.w);
-      if constexpr (FEED == kFeedReg) {
-        ra[j] = shift_tile(lt, ra[j]) ^ c;
-      } else if constexpr (FEED == kFeedLds) {
-        uint32_t* a = la + j * kBlock + threadIdx.x;
-        *a = shift_tile(lt, *a) ^ c;
+      if constexpr (NB == 4) {
+        if constexpr (FEED == kFeedReg) {
+          ra[j] = pre_step<LAST>(lt, ra[j], x.x, x.y, x.z, x.w);
+        } else if constexpr (FEED == kFeedLds) {
+          uint32_t* a = la + j * las + threadIdx.x;
+          *a = pre_step<LAST>(lt, *a, x.x, x.y, x.z, x.w);
+        } else {
+          tail[static_cast<size_t>(j) * kBlock + tid] = pre_step<true>(lt, 0u, x.x, x.y, x.z, x.w);
+        }
       } else {
-        tail[static_cast<size_t>(j) * kBlock + threadIdx.x] = c;
+        const uint32_t c = chunk_crc(lt, x);
+        if constexpr (FEED == kFeedReg) {
+          ra[j] = shift_tile(lt, ra[j]) ^ c;
+        } else if constexpr (FEED == kFeedLds) {
+          uint32_t* a = la + j * las + threadIdx.x;
+          *a = shift_tile(lt, *a) ^ c;
+        } else {
+          tail[static_cast<size_t>(j) * kBlock + tid] = c;
+        }
       }
     }
   }
@@ -435,23 +453,54 @@ constexpr int crc_waves() {
 // from those sources' chains instead of per tile. (A compile-time choice: a
 // runtime row mask inside the tile loop costs the register-tight kernel its
 // registers.)
-// NB: dwords of each chunk through the byte tables (chunk_crc_nb).
-template <int P, class Pol, bool REG, bool SRC, bool X0 = false, int NB = 0>
-__global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_encode_crc_v16(
+// NB = 4: pre-shifted chains through the byte-position tables (pre_step);
+// NB = 0: 5-bit field tables and a Z^4096 step per tile.
+// NV: independent 256-lane groups per workgroup sharing one LDS copy of the
+// tables (no barrier after the table load); the per-lane source chains then
+// set how many waves fit a CU.
+template <int P, class Pol, bool REG, bool SRC, bool X0 = false, int NB = 0, int NV = 1>
+__global__ __launch_bounds__(kBlock * NV, (crc_waves<P, Pol::U, REG>())) void ec_encode_crc_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned nblk, unsigned tt,
     unsigned nfull, unsigned ntiles, unsigned long long x0src, const uint32_t* __restrict__ tabs,
     uint32_t* __restrict__ part, uint32_t* __restrict__ tail, int nshard_total, int out_shard0) {
   static_assert(!X0 || SRC, "row 0 is derived from this pass's source chains");
+  static_assert(NB == 0 || NB == 4, "byte path: all four dwords");
   constexpr int kFull = SRC ? (REG ? kFeedReg : kFeedLds) : kFeedNone;
   constexpr int kRag = SRC ? kFeedTail : kFeedNone;
   constexpr int NR = REG ? Pol::U : 1;
-  __shared__ uint32_t lt[kCrcTabDw + NB * 1024];
-  extern __shared__ uint32_t la[];  // [k][kBlock] when SRC && !REG
-  if constexpr (NB > 0)
-    for (int i = threadIdx.x; i < NB * 1024; i += kBlock) lt[kB16 + i] = tabs[ISAL_HIP_CRC_B16_TAB + i];
-  load_crc_tables(lt, tabs);  // (its barrier covers the byte tables too)
-  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+  constexpr unsigned kLa = kBlock * NV;
+  __shared__ uint32_t lt[NB ? kPosLds : kCrcTabDw];
+  extern __shared__ uint32_t la[];  // [k][kBlock * NV] when SRC && !REG
+  if constexpr (NB) {
+    const uint4* src = reinterpret_cast<const uint4*>(tabs + ISAL_HIP_CRC_B16_TAB);
+    for (int i = threadIdx.x; i < kPosLds / 4; i += kBlock * NV) reinterpret_cast<uint4*>(lt)[i] = src[i];
+    __syncthreads();
+  } else {
+    load_crc_tables(lt, tabs);
+  }
+  const unsigned tid = threadIdx.x % kBlock;
+  // parity chain step and chunk CRC of the parity's ragged tile
+  auto pstep = [&](auto lastc, uint32_t a, const uint32_t (&v)[4]) __attribute__((always_inline)) {
+    if constexpr (NB)
+      return pre_step<decltype(lastc)::value>(lt, a, v[0], v[1], v[2], v[3]);
+    else
+      return shift_tile(lt, a) ^ chunk_crc(lt, v[0], v[1], v[2], v[3]);
+  };
+  auto pchunk = [&](const uint32_t (&v)[4]) __attribute__((always_inline)) {
+    if constexpr (NB)
+      return pre_step<true>(lt, 0u, v[0], v[1], v[2], v[3]);
+    else
+      return chunk_crc(lt, v[0], v[1], v[2], v[3]);
+  };
+  // the last full tile of a block takes the LAST variant (uniform branch)
+  auto with_last = [&](bool last, auto&& body) __attribute__((always_inline)) {
+    if (last)
+      body(std::integral_constant<bool, true>{});
+    else
+      body(std::integral_constant<bool, false>{});
+  };
+  for (unsigned w = blockIdx.x * NV + threadIdx.x / kBlock; w < nitems; w += gridDim.x * NV) {
     const unsigned stripe = w / nblk, blk = w - stripe * nblk;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const size_t shard_s = static_cast<size_t>(stripe) * nshard_total;  // source shard 0
@@ -463,16 +512,25 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
 #pragma unroll
     for (int j = 0; j < NR; ++j) ra[j] = 0;
     if constexpr (SRC && !REG)
-      for (int j = 0; j < k; ++j) la[j * kBlock + threadIdx.x] = 0;
+      for (int j = 0; j < k; ++j) la[j * kLa + threadIdx.x] = 0;
+    auto store_and_chain = [&](auto lastc, uint32_t (&acc)[P][4], long long off)
+                               __attribute__((always_inline)) {
+#pragma unroll
+      for (int l = 0; l < P; ++l) {
+        store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
+                         len);
+        if (!(X0 && l == 0)) ao[l] = pstep(lastc, ao[l], acc[l]);
+      }
+    };
     if constexpr (REG) {
       // Software pipeline: the next tile's sources are in flight while this
       // tile's GF and CRC work runs (the CRC lookups otherwise leave HBM idle).
       uint4 xn[Pol::U];
       if (t0 < tf)
-        load_group<Pol::U, Pol::LD>(xn, sp + src0, 0, static_cast<long long>(t0) * kTile + threadIdx.x * kVec,
+        load_group<Pol::U, Pol::LD>(xn, sp + src0, 0, static_cast<long long>(t0) * kTile + tid * kVec,
                                     len);
       for (unsigned t = t0; t < tf; ++t) {
-        const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
+        const long long off = static_cast<long long>(t) * kTile + tid * kVec;
         uint4 x[Pol::U];
 #pragma unroll
         for (int u = 0; u < Pol::U; ++u) x[u] = xn[u];
@@ -482,41 +540,36 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
         for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
         int z = 0;  // opaque zero: see below
         asm volatile("" : "+s"(z));
-        mac_feed16<P, Pol::U>(acc, x, 0, tbl + z, SrcFeed<kFull, NB>{lt, la, ra, tail + shard_s * kBlock});
-#pragma unroll
-        for (int l = 0; l < P; ++l) {
-          store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
-                           len);
-          if (!(X0 && l == 0))
-            ao[l] = shift_tile(lt, ao[l]) ^ chunk_crc_nb<NB>(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
-        }
+        with_last(t + 1 == tf, [&](auto lastc) __attribute__((always_inline)) {
+          mac_feed16<P, Pol::U>(acc, x, 0, tbl + z,
+                                SrcFeed<kFull, NB, decltype(lastc)::value>{
+                                    lt, la, ra, tail + shard_s * kBlock, kLa, tid});
+          store_and_chain(lastc, acc, off);
+        });
       }
     } else {
       for (unsigned t = t0; t < tf; ++t) {
-        const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
+        const long long off = static_cast<long long>(t) * kTile + tid * kVec;
         uint32_t acc[P][4];
         // An opaque zero offset per tile keeps the compiler from hoisting all
         // k*P*5 coefficient dwords out of the tile loop (that spills SGPRs).
         int z = 0;
         asm volatile("" : "+s"(z));
-        accum16_crc<P, Pol, REG>(acc, sp + src0, tbl + z, k, off, len,
-                                 SrcFeed<kFull, NB>{lt, la, ra, tail + shard_s * kBlock});
-#pragma unroll
-        for (int l = 0; l < P; ++l) {
-          store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
-                           len);
-          if (!(X0 && l == 0))
-            ao[l] = shift_tile(lt, ao[l]) ^ chunk_crc_nb<NB>(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
-        }
+        with_last(t + 1 == tf, [&](auto lastc) __attribute__((always_inline)) {
+          accum16_crc<P, Pol, REG>(acc, sp + src0, tbl + z, k, off, len,
+                                   SrcFeed<kFull, NB, decltype(lastc)::value>{
+                                       lt, la, ra, tail + shard_s * kBlock, kLa, tid});
+          store_and_chain(lastc, acc, off);
+        });
       }
     }
     if (tf < t1) {  // the ragged last tile (t == nfull): len % 16 == 0 here
-      const long long off = static_cast<long long>(tf) * kTile + threadIdx.x * kVec;
+      const long long off = static_cast<long long>(tf) * kTile + tid * kVec;
       uint32_t* trow = tail + shard_s * kBlock;
       if (off + kVec <= len) {
         uint32_t acc[P][4];
         accum16_crc<P, Pol, REG>(acc, sp + src0, tbl, k, off, len,
-                                 SrcFeed<kRag>{lt, la, ra, trow});
+                                 SrcFeed<kRag, NB>{lt, la, ra, trow, kLa, tid});
 #pragma unroll
         for (int l = 0; l < P; ++l) {
           store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
@@ -524,17 +577,17 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
           uint32_t c = 0;
           if (X0 && l == 0) {  // the sources' tail chunks: this lane wrote them above
             for (int j = 0; j < k; ++j)
-              if ((x0src >> j) & 1ull) c ^= trow[j * kBlock + threadIdx.x];
+              if ((x0src >> j) & 1ull) c ^= trow[j * kBlock + tid];
           } else {
-            c = chunk_crc(lt, acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+            c = pchunk(acc[l]);
           }
-          trow[(out_shard0 + l) * kBlock + threadIdx.x] = c;
+          trow[(out_shard0 + l) * kBlock + tid] = c;
         }
       } else {  // lane past len
         if constexpr (SRC)
-          for (int j = 0; j < k; ++j) trow[j * kBlock + threadIdx.x] = 0;
+          for (int j = 0; j < k; ++j) trow[j * kBlock + tid] = 0;
 #pragma unroll
-        for (int l = 0; l < P; ++l) trow[(out_shard0 + l) * kBlock + threadIdx.x] = 0;
+        for (int l = 0; l < P; ++l) trow[(out_shard0 + l) * kBlock + tid] = 0;
       }
     }
     if constexpr (X0) {  // row 0's chain = XOR of its sources' chains
@@ -545,20 +598,20 @@ __global__ __launch_bounds__(kBlock, (crc_waves<P, Pol::U, REG>())) void ec_enco
           if ((x0src >> j) & 1ull) v ^= ra[j];
       } else {
         for (int j = 0; j < k; ++j)
-          if ((x0src >> j) & 1ull) v ^= la[j * kBlock + threadIdx.x];
+          if ((x0src >> j) & 1ull) v ^= la[j * kLa + threadIdx.x];
       }
       ao[0] = v;
     }
 #pragma unroll
     for (int l = 0; l < P; ++l)
-      part[((shard_s + out_shard0 + l) * nblk + blk) * kBlock + threadIdx.x] = ao[l];
+      part[((shard_s + out_shard0 + l) * nblk + blk) * kBlock + tid] = ao[l];
     if constexpr (SRC) {
       if constexpr (REG) {
 #pragma unroll
-        for (int j = 0; j < NR; ++j) part[((shard_s + j) * nblk + blk) * kBlock + threadIdx.x] = ra[j];
+        for (int j = 0; j < NR; ++j) part[((shard_s + j) * nblk + blk) * kBlock + tid] = ra[j];
       } else {
         for (int j = 0; j < k; ++j)
-          part[((shard_s + j) * nblk + blk) * kBlock + threadIdx.x] = la[j * kBlock + threadIdx.x];
+          part[((shard_s + j) * nblk + blk) * kBlock + tid] = la[j * kLa + threadIdx.x];
       }
     }
   }
@@ -595,27 +648,43 @@ int crc_byte_dwords() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC_BYTE_DWORDS) == 0 ? 0 : 4;
 }
 
+// 256-lane groups per workgroup of the byte-path kernel with LDS source
+// chains: 2 when that fits more groups on a CU (160 KiB of LDS: 32 KiB of
+// tables per workgroup, 1 KiB of chains per source and group), else 1;
+// ISAL_HIP_CRC_FUSED_NV = 1 or 2 forces it where it fits.
+int fused_nv32(int k) {
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC_FUSED_NV);
+  const size_t cap = 160 * 1024, tabs = kPosLds * 4, la = static_cast<size_t>(k) * kBlock * 4;
+  if (tabs + 2 * la > cap) return 1;
+  if (v == 1 || v == 2) return static_cast<int>(v);
+  return 2 * (cap / (tabs + 2 * la)) > cap / (tabs + la) ? 2 : 1;
+}
+
 template <int P, int U>
 void launch_fused(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
                   int src0, int dst0, const uint32_t* tbl, int len, int k, unsigned nitems,
                   const isal_hip_crc_geom& g, const isal_hip_xrows& xr, const uint32_t* tabs,
                   uint32_t* part, uint32_t* tail, int nshard_total, int crc_src, int out_shard0) {
-#define FUSED_LAUNCH(REG, SRC, X0, LDS, NB)                                                      \
-  hipLaunchKernelGGL((ec_encode_crc_v16<P, FusedPol<U>, REG, SRC, X0, NB>), dim3(grid), dim3(kBlock), \
-                     LDS, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems,                    \
-                     static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),                   \
-                     static_cast<unsigned>(g.nfull), static_cast<unsigned>(g.ntiles), xr.src[0],  \
-                     tabs, part, tail, nshard_total, out_shard0)
+#define FUSED_LAUNCH(REG, SRC, X0, LDS, NB, NV)                                                  \
+  hipLaunchKernelGGL((ec_encode_crc_v16<P, FusedPol<U>, REG, SRC, X0, NB, NV>),                   \
+                     dim3((grid + NV - 1) / NV), dim3(kBlock * NV), (LDS) * NV, s, ptrs, ptr_stride, \
+                     src0, dst0, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),               \
+                     static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull),                  \
+                     static_cast<unsigned>(g.ntiles), xr.src[0], tabs, part, tail, nshard_total,   \
+                     out_shard0)
   const bool x0 = crc_src && (xr.rows & 1u);
   const bool nb4 = crc_byte_dwords() == 4;
+  const bool nv2 = nb4 && crc_src && fused_nv32(k) == 2;
   if (!crc_src)
-    FUSED_LAUNCH(false, false, false, 0, 0);
+    FUSED_LAUNCH(false, false, false, 0, 0, 1);
   else if (k == U && src_chain_reg())  // one load group: source chains in registers (no X0:
-    FUSED_LAUNCH(true, true, false, 0, 0);  // its 2 extra SGPRs make the register variant spill)
-  else if (x0) {
-    if (nb4) FUSED_LAUNCH(false, true, true, lds, 4); else FUSED_LAUNCH(false, true, true, lds, 0);
+    FUSED_LAUNCH(true, true, false, 0, 0, 1);  // its 2 extra SGPRs make the register variant spill)
+  else if (!nb4) {
+    if (x0) FUSED_LAUNCH(false, true, true, lds, 0, 1); else FUSED_LAUNCH(false, true, false, lds, 0, 1);
+  } else if (nv2) {
+    if (x0) FUSED_LAUNCH(false, true, true, lds, 4, 2); else FUSED_LAUNCH(false, true, false, lds, 4, 2);
   } else {
-    if (nb4) FUSED_LAUNCH(false, true, false, lds, 4); else FUSED_LAUNCH(false, true, false, lds, 0);
+    if (x0) FUSED_LAUNCH(false, true, true, lds, 4, 1); else FUSED_LAUNCH(false, true, false, lds, 4, 1);
   }
 #undef FUSED_LAUNCH
 }

@@ -107,6 +107,7 @@ enum {
         ISAL_HIP_KNOB_CRC64_SLICE,     /* fused encode+CRC64 chunk path: fields(0) | slice8(1) */
         ISAL_HIP_KNOB_CRC64_FUSED_NV,  /* 256-lane groups per fused encode+CRC64 workgroup: 1 | 2 */
         ISAL_HIP_KNOB_CRC_BYTE_DWORDS, /* fused encode+CRC32C: chunk dwords via byte tables, 0 | 4 */
+        ISAL_HIP_KNOB_CRC_FUSED_NV,    /* 256-lane groups per fused encode+CRC32C workgroup: 1 | 2 */
         ISAL_HIP_KNOB_FAULT,           /* fault-injection site of GPU-routed calls (tests) */
         ISAL_HIP_KNOB_COUNT
 };
@@ -150,11 +151,13 @@ unsigned long long isal_cpu_run(int op, long long c0, int len, int k, int rows, 
 #define ISAL_HIP_CRC_CHUNK_DWORDS (4 * ISAL_HIP_CRC_FIELDS * 32)
 #define ISAL_HIP_CRC_EXT_TAB (ISAL_HIP_CRC_TAB_DWORDS + ISAL_HIP_CRC_PLAN_DWORDS)
 #define ISAL_HIP_CRC_EXT_DWORDS (3 * ISAL_HIP_CRC_CHUNK_DWORDS + ISAL_HIP_CRC_FIELDS * 32)
-/* Byte-position tables of crc(0, 16-byte chunk) after EXT: table p (byte p of
- * the chunk) = crc of byte b followed by 15 - p zero bytes, 16 x 256 dwords
- * (the fused kernel's byte-indexed chunk path). */
+/* Byte-position tables of the fused kernel's byte path, after EXT:
+ *   P:  table p (byte p of a 16-byte chunk) = crc of byte b followed by
+ *       15 - p zero bytes, 16 x 256 dwords;
+ *   P': the same followed by 4080 more zero bytes (Z^4080 o P: the step of a
+ *       pre-shifted chain, crc_kernels.hip). */
 #define ISAL_HIP_CRC_B16_TAB (ISAL_HIP_CRC_EXT_TAB + ISAL_HIP_CRC_EXT_DWORDS)
-#define ISAL_HIP_CRC_B16_DWORDS (16 * 256)
+#define ISAL_HIP_CRC_B16_DWORDS (2 * 16 * 256)
 void isal_hip_crc32c_byte_tables(uint32_t *out);
 #define ISAL_HIP_CRC_MAX_FUSED_K 64 /* fused encode keeps k source partials in LDS */
 
@@ -186,9 +189,9 @@ typedef struct {
  *              path, in the "u-domain" u = pi(s) (pi = byte swap for the norm
  *              flavours, identity for refl), where processing 8 bytes d is
  *              u' = A(d ^ u) for every flavour:
- *                A_j[v] = pi(raw(0, v at byte j of 8)),  8 x 256
- *                B_j[v] = pi(Z^4096 raw(0, v at byte j of 8)), 8 x 256
- *   UOP_TAB    pi Z^4096 pi, pi Z^8192 pi (u-domain chain steps, field tables) */
+ *                A_j[v]  = pi(raw(0, v at byte j of 8)),  8 x 256
+ *                A'_j[v] = pi(Z^4080 raw(0, v at byte j of 8)), 8 x 256
+ *              (A' advances a lane's chain past the rest of its tile) */
 #define ISAL_HIP_CRC64_OP_ENTRIES (2 * ISAL_HIP_CRC_FIELDS * 32)
 #define ISAL_HIP_CRC64_BYTE_TAB 0
 #define ISAL_HIP_CRC64_CHUNK_TAB 256
@@ -203,8 +206,7 @@ typedef struct {
 #define ISAL_HIP_CRC64_SHIFTX_TAB (ISAL_HIP_CRC64_CHUNKX_TAB + 3 * ISAL_HIP_CRC64_CHUNK_ENTRIES)
 #define ISAL_HIP_CRC64_SLICE_TAB (ISAL_HIP_CRC64_SHIFTX_TAB + 2 * ISAL_HIP_CRC64_OP_ENTRIES)
 #define ISAL_HIP_CRC64_SLICE_ENTRIES (2 * 8 * 256)
-#define ISAL_HIP_CRC64_UOP_TAB (ISAL_HIP_CRC64_SLICE_TAB + ISAL_HIP_CRC64_SLICE_ENTRIES)
-#define ISAL_HIP_CRC64_TAB_ENTRIES (ISAL_HIP_CRC64_UOP_TAB + 2 * ISAL_HIP_CRC64_OP_ENTRIES)
+#define ISAL_HIP_CRC64_TAB_ENTRIES (ISAL_HIP_CRC64_SLICE_TAB + ISAL_HIP_CRC64_SLICE_ENTRIES)
 
 typedef struct {
         long long nfull;      /* full 4 KiB tiles */
