@@ -646,7 +646,17 @@ def main(argv=None):
                 reg = k == u and os.environ.get("ISAL_HIP_CRC_SRC_CHAIN") == "reg"
                 x0 = "false" if reg else "true"  # Vandermonde row 0 derived (LDS-chain variant)
                 nb = 0 if reg or os.environ.get("ISAL_HIP_CRC_BYTE_DWORDS") == "0" else 4  # byte tables
-                kernel = f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true, {x0}, {nb}>"
+                # lane groups per workgroup: the launcher's rule (crc_kernels.hip fused_nv32)
+                tabs_b, la_b, cap = 32 * 256 * 4, k * 256 * 4, 160 * 1024
+                nv_env = os.environ.get("ISAL_HIP_CRC_FUSED_NV")
+                if not nb or tabs_b + 2 * la_b > cap:
+                    nv = 1
+                elif nv_env in ("1", "2"):
+                    nv = int(nv_env)
+                else:
+                    nv = 2 if 2 * (cap // (tabs_b + 2 * la_b)) > cap // (tabs_b + la_b) else 1
+                kernel = (f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true, {x0}, "
+                          f"{nb}, {nv}>")
                 workload = (f"C2 encode + CRC32C (crc32_iscsi) of all k+p shards in one pass: k={k} "
                             f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
             else:

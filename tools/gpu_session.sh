@@ -107,6 +107,24 @@ for s in $STEPS; do
                         done
                 done
                 ;;
+        memprobe)
+                # memory-only kernels with the encode addressing: C2 (10 read + 4 write) and C3 decode (10 + 3)
+                run probe_c2 300 isa-l_amd/build/ec_probe 10 4 1048576 1024 5
+                run probe_c3 300 isa-l_amd/build/ec_probe 10 3 1048576 1024 5
+                ;;
+        fusedprof)
+                # kernel stats of the fused encode+CRC kernels (default paths) for the roofline lines
+                run rocprof_encrc 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_encrc" -o encrc -- python3 bench.py --workload encode-crc --no-cpu-baseline
+                run rocprof_encrc64 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_encrc64" -o encrc64 -- python3 bench.py --workload encode-crc64 --no-cpu-baseline
+                for wl in encode-crc encode-crc64; do
+                        run pmc_fetch_$wl 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$wl" -o f -- python3 bench.py --workload $wl --no-cpu-baseline --steps 3 --warmup 1
+                        run pmc_write_$wl 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$wl" -o w -- python3 bench.py --workload $wl --no-cpu-baseline --steps 3 --warmup 1
+                done
+                python3 tools/pmc_csv.py "$OUT/pmc_c2_encode_crc.csv" "workload=encode-crc k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode-crc --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encode-crc" "$OUT/pmc_write_encode-crc" ec_encode_crc_v16
+                python3 tools/pmc_csv.py "$OUT/pmc_c2_encode_crc64.csv" "workload=encode-crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode-crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encode-crc64" "$OUT/pmc_write_encode-crc64" ec_encode_crc64_v16
+                run bench_encode_crc 300 python bench.py --workload encode-crc --cpu-seconds 5
+                run bench_encode_crc64 300 python bench.py --workload encode-crc64 --cpu-seconds 5
+                ;;
         encrc64sweep)
                 for cfg in ${ENCRC64_CFGS:-reg:10 lds:10 lds:5}; do
                         ISAL_HIP_CRC64_SRC_CHAIN=${cfg%:*} ISAL_HIP_CRC64_FUSED_U=${cfg#*:} run bench_encrc64_${cfg/:/_u} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
