@@ -243,6 +243,17 @@ isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
         isal_hip_crc64_zpow(variant, (unsigned long long) (g.tail / 16) * 16, m);
         op_tables(m, tabs + ISAL_HIP_CRC64_OP_TAIL);
         slice_tables(variant, tabs);
+        /* pre-shifted field tables (u-domain) of the checksum-only kernel */
+        isal_hip_crc64_zpow(variant, ISAL_HIP_CRC_TILE - 16, m);
+        {
+                uint64_t bu[128], bz[128];
+                for (j = 0; j < 128; j++) {
+                        bu[j] = pi_of(variant, basis[j]);
+                        bz[j] = pi_of(variant, apply(m, basis[j]));
+                }
+                chunk_tables(bu, tabs + ISAL_HIP_CRC64_PRE_TAB);
+                chunk_tables(bz, tabs + ISAL_HIP_CRC64_PRE_TAB + ISAL_HIP_CRC64_CHUNK_ENTRIES);
+        }
 }
 
 void

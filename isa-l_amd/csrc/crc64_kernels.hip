@@ -222,6 +222,62 @@ __global__ __launch_bounds__(kBlock) void crc64_shards(const uint64_t* __restric
   }
 }
 
+// Pre-shifted chains (the fused kernel's idea, crc64_kernels.hip SL path) on
+// conflict-free 5-bit field tables: a lane keeps b = Z^4080_u(a) in the
+// u-domain, XORs it into the next chunk's first 8 bytes like a CRC register and
+// maps the chunk once, b' = F'_u(chunk ^ b) — 28 lookups per tile and no chain
+// step (M = 2 spends 35) — the item's last tile applies F_u and leaves the
+// plain chain. Loads are double-buffered (the next B tiles in flight).
+template <int B>
+__global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __restrict__ ptrs,
+                                                           int ptr_stride, int nsh, int len,
+                                                           unsigned nitems, unsigned nblk,
+                                                           unsigned tt, unsigned nfull, int uswap,
+                                                           const uint64_t* __restrict__ tabs,
+                                                           uint64_t* __restrict__ part) {
+  __shared__ uint64_t lt[2 * kCE];  // F_u, F'_u
+  load_lds<2 * kCE>(lt, tabs + ISAL_HIP_CRC64_PRE_TAB);
+  __syncthreads();
+  const long long lane = threadIdx.x * kVec;
+  auto step = [&](unsigned t, unsigned t1, X64 b, const uint4& x) __attribute__((always_inline)) {
+    X64 c{0u, 0u};
+    if (t + 1 == t1)
+      chunk_acc(c, lt, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
+    else
+      chunk_acc(c, lt + kCE, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
+    return c;
+  };
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned si = w / nblk, blk = w - si * nblk;
+    const unsigned stripe = si / nsh, i = si - stripe * nsh;
+    const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
+    const unsigned t0 = blk * tt, t1 = t0 + tt < nfull ? t0 + tt : nfull;
+    X64 b{0u, 0u};
+    unsigned t = t0;
+    uint4 xn[B];
+    if (t + B <= t1) {
+#pragma unroll
+      for (int g = 0; g < B; ++g) xn[g] = load16<kBufNT>(base, static_cast<long long>(t + g) * kTile + lane, len);
+    }
+    for (; t + B <= t1; t += B) {
+      uint4 x[B];
+#pragma unroll
+      for (int g = 0; g < B; ++g) x[g] = xn[g];
+      if (t + 2 * B <= t1) {
+#pragma unroll
+        for (int g = 0; g < B; ++g)
+          xn[g] = load16<kBufNT>(base, static_cast<long long>(t + B + g) * kTile + lane, len);
+      }
+#pragma unroll
+      for (int g = 0; g < B; ++g) b = step(t + g, t1, b, x[g]);
+    }
+    for (; t < t1; ++t)
+      b = step(t, t1, b, load16<kBufNT>(base, static_cast<long long>(t) * kTile + lane, len));
+    const uint64_t a = b.get();
+    part[static_cast<size_t>(w) * kBlock + threadIdx.x] = uswap ? __builtin_bswap64(a) : a;
+  }
+}
+
 // v(L) <- sum over lanes of Z^(16 * (255 - L)) v(L), result in red[0]:
 // 8 levels, level s joins lanes L and L + 2^s with Z^(16 * 2^s).
 __device__ __forceinline__ uint64_t lane_tree(uint64_t* red, const uint64_t* tree) {
@@ -300,6 +356,12 @@ constexpr unsigned long long kMaxItems = 1ull << 30;
 int chain_step() {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_STEP);
   return v == 1 || v == 4 ? static_cast<int>(v) : 2;
+}
+
+// Pre-shifted chains in the standalone kernel (ISAL_HIP_CRC_PRE=0: the
+// chain-step kernels above, with ISAL_HIP_CRC64_STEP / _BATCH).
+bool shards_pre() {
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC_PRE) != 0;
 }
 
 // Full tiles loaded per batch (ISAL_HIP_CRC64_BATCH = 4 or 8).
@@ -765,7 +827,12 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
                      len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),      \
                      static_cast<unsigned>(g.nfull), d_tabs, part)
       const int m = chain_step(), b8 = load_batch() == 8;
-      if (!vec16)
+      if (vec16 && shards_pre())
+        hipLaunchKernelGGL(crc64_shards_pre<4>, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride,
+                           nsh, len, nitems, static_cast<unsigned>(g.nblk),
+                           static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), !refl,
+                           d_tabs, part);
+      else if (!vec16)
         SHARDS_LAUNCH(false, 1, 4);
       else if (m == 4)
         { if (b8) SHARDS_LAUNCH(true, 4, 8); else SHARDS_LAUNCH(true, 4, 4); }

@@ -155,6 +155,17 @@ isal_hip_crc32c_byte_tables(uint32_t *out)
                 }
 }
 
+/* F' (ISAL_HIP_CRC_FPRE_TAB): every entry of the chunk field tables shifted by
+ * 4080 zero bytes. */
+void
+isal_hip_crc32c_pre_tables(const uint32_t *tabs, uint32_t *out)
+{
+        const uint32_t z = isal_hip_crc32c_xpow8n(ISAL_HIP_CRC_TILE - ISAL_HIP_CRC_SLICES);
+        int e;
+        for (e = 0; e < ISAL_HIP_CRC_CHUNK_DWORDS; e++)
+                out[e] = isal_hip_crc32c_mulmod(tabs[ISAL_HIP_CRC_CHUNK_TAB + e], z);
+}
+
 /* Tables of the multi-tile chain step from the base tables: every entry of a
  * chunk map shifted by m tiles is entry * x^(8*4096*m) mod P; Z^(4096*4) of a
  * field value is its Z^4096 entry shifted by three more tiles. */

@@ -273,6 +273,74 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards(
   }
 }
 
+// Pre-shifted chains on the conflict-free field tables (see pre_step): a lane
+// keeps b = Z^4080(a), XORs it into the next chunk's first dword like a CRC
+// register and maps the chunk once, b' = F'(w0 ^ b, w1, w2, w3) — 28 lookups
+// per tile and no Z^4096 step (35 before) — the block's last full tile applies
+// F (crc(0, chunk)) and leaves the plain chain. Double-buffered loads as above.
+// LDS: T0 (tail bytes), F (the CHUNK tables), F' (ISAL_HIP_CRC_FPRE_TAB).
+constexpr int kPreF = ISAL_HIP_CRC_CHUNK_TAB, kPreFZ = kPreF + ISAL_HIP_CRC_CHUNK_DWORDS;
+
+__global__ __launch_bounds__(kBlock) void crc32c_shards_pre(
+    const uint64_t* __restrict__ ptrs, int ptr_stride, int idx0, int nsh, int len,
+    unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, unsigned ntiles,
+    const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part, uint32_t* __restrict__ tail,
+    int nshard_total, int shard0) {
+  __shared__ uint32_t lt[kPreFZ + ISAL_HIP_CRC_CHUNK_DWORDS];
+  for (int i = threadIdx.x; i < kPreFZ; i += kBlock) lt[i] = tabs[i];
+  for (int i = threadIdx.x; i < ISAL_HIP_CRC_CHUNK_DWORDS; i += kBlock)
+    lt[kPreFZ + i] = tabs[ISAL_HIP_CRC_FPRE_TAB + i];
+  __syncthreads();
+  const long long lane = threadIdx.x * kVec;
+  auto step = [&](unsigned t, unsigned tf, uint32_t b, const uint4& x) __attribute__((always_inline)) {
+    return t + 1 == tf ? chunk_map(lt + kPreF, x.x ^ b, x.y, x.z, x.w)
+                       : chunk_map(lt + kPreFZ, x.x ^ b, x.y, x.z, x.w);
+  };
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned si = w / nblk, blk = w - si * nblk;
+    const unsigned stripe = si / nsh, i = si - stripe * nsh;
+    const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + idx0 + i];
+    const size_t shard = static_cast<size_t>(stripe) * nshard_total + shard0 + i;
+    const unsigned t0 = blk * tt, t1 = t0 + tt < ntiles ? t0 + tt : ntiles;
+    const unsigned tf = t1 < nfull ? t1 : nfull;  // full tiles of this block
+    uint32_t b = 0;
+    unsigned t = t0;
+    uint4 xn[kCrcBatch];
+    if (t + kCrcBatch <= tf) {
+#pragma unroll
+      for (unsigned g = 0; g < kCrcBatch; ++g)
+        xn[g] = load16<kBufNT>(base, static_cast<long long>(t + g) * kTile + lane, len);
+    }
+    for (; t + kCrcBatch <= tf; t += kCrcBatch) {
+      uint4 x[kCrcBatch];
+#pragma unroll
+      for (unsigned g = 0; g < kCrcBatch; ++g) x[g] = xn[g];
+      if (t + 2 * kCrcBatch <= tf) {
+#pragma unroll
+        for (unsigned g = 0; g < kCrcBatch; ++g)
+          xn[g] = load16<kBufNT>(base, static_cast<long long>(t + kCrcBatch + g) * kTile + lane, len);
+      }
+#pragma unroll
+      for (unsigned g = 0; g < kCrcBatch; ++g) b = step(t + g, tf, b, x[g]);
+    }
+    for (; t < tf; ++t) b = step(t, tf, b, load16<kBufNT>(base, static_cast<long long>(t) * kTile + lane, len));
+    if (tf < t1) {  // the ragged tile: its chunk CRCs go to tail[]
+      const long long off = static_cast<long long>(tf) * kTile + lane;
+      const long long left = len - off;
+      const int nb = left >= kVec ? kVec : (left > 0 ? static_cast<int>(left) : 0);
+      uint32_t c = 0;
+      if (nb == kVec) {
+        const uint4 x = load16<kBufNT>(base, off, len);
+        c = chunk_map(lt + kPreF, x.x, x.y, x.z, x.w);
+      } else if (nb > 0) {
+        c = bytes_crc(lt, reinterpret_cast<const uint8_t*>(base) + off, nb);
+      }
+      tail[shard * kBlock + threadIdx.x] = c;
+    }
+    part[(shard * nblk + blk) * kBlock + threadIdx.x] = b;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Combine: one workgroup per shard (grid-stride). Lane L folds its partials of
 // every block (Horner with the byte tables of x^(8*4096*tt); the last block
@@ -315,6 +383,12 @@ constexpr unsigned kMaxCrcItems = 1u << 30;
 // Tiles per chain step of crc32c_shards (ISAL_HIP_CRC_STEP = 1 or 4). Unlike
 // CRC64 the CRC32C kernel is not bound by its lookups: step 4 measured 2.90 ms
 // vs 2.87 ms per C2 step (profiles/r01_crc_step_sweep.txt), so 1 by default.
+// Pre-shifted chains in the checksum-only kernel (ISAL_HIP_CRC_PRE=0: the
+// chain-step kernel, with ISAL_HIP_CRC_STEP).
+bool crc_pre() {
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC_PRE) != 0;
+}
+
 int crc_step() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC_STEP) == 4 ? 4 : 1;
 }
@@ -760,7 +834,12 @@ extern "C" int isal_hip_launch_crc(const uint64_t* d_ptrs, int ptr_stride, int i
                      ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),           \
                      static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),                   \
                      static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0)
-    if (!vec16)
+    if (vec16 && crc_pre())
+      hipLaunchKernelGGL(crc32c_shards_pre, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
+                         ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
+                         static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
+                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
+    else if (!vec16)
       CRC_SHARDS(false, 1);
     else if (crc_step() == 4)
       CRC_SHARDS(true, 4);

@@ -108,6 +108,7 @@ enum {
         ISAL_HIP_KNOB_CRC64_FUSED_NV,  /* 256-lane groups per fused encode+CRC64 workgroup: 1 | 2 */
         ISAL_HIP_KNOB_CRC_BYTE_DWORDS, /* fused encode+CRC32C: chunk dwords via byte tables, 0 | 4 */
         ISAL_HIP_KNOB_CRC_FUSED_NV,    /* 256-lane groups per fused encode+CRC32C workgroup: 1 | 2 */
+        ISAL_HIP_KNOB_CRC_PRE,         /* checksum-only CRC32C/CRC64 kernels: pre-shifted chains (default) | 0 */
         ISAL_HIP_KNOB_FAULT,           /* fault-injection site of GPU-routed calls (tests) */
         ISAL_HIP_KNOB_COUNT
 };
@@ -159,6 +160,11 @@ unsigned long long isal_cpu_run(int op, long long c0, int len, int k, int rows, 
 #define ISAL_HIP_CRC_B16_TAB (ISAL_HIP_CRC_EXT_TAB + ISAL_HIP_CRC_EXT_DWORDS)
 #define ISAL_HIP_CRC_B16_DWORDS (2 * 16 * 256)
 void isal_hip_crc32c_byte_tables(uint32_t *out);
+/* F' = Z^4080 o crc(0, chunk) as field tables (the layout of CHUNK_TAB), for
+ * the checksum-only kernel's pre-shifted chains. */
+#define ISAL_HIP_CRC_FPRE_TAB (ISAL_HIP_CRC_B16_TAB + ISAL_HIP_CRC_B16_DWORDS)
+#define ISAL_HIP_CRC_FPRE_DWORDS ISAL_HIP_CRC_CHUNK_DWORDS
+void isal_hip_crc32c_pre_tables(const uint32_t *tabs, uint32_t *out);
 #define ISAL_HIP_CRC_MAX_FUSED_K 64 /* fused encode keeps k source partials in LDS */
 
 typedef struct {
@@ -206,7 +212,10 @@ typedef struct {
 #define ISAL_HIP_CRC64_SHIFTX_TAB (ISAL_HIP_CRC64_CHUNKX_TAB + 3 * ISAL_HIP_CRC64_CHUNK_ENTRIES)
 #define ISAL_HIP_CRC64_SLICE_TAB (ISAL_HIP_CRC64_SHIFTX_TAB + 2 * ISAL_HIP_CRC64_OP_ENTRIES)
 #define ISAL_HIP_CRC64_SLICE_ENTRIES (2 * 8 * 256)
-#define ISAL_HIP_CRC64_TAB_ENTRIES (ISAL_HIP_CRC64_SLICE_TAB + ISAL_HIP_CRC64_SLICE_ENTRIES)
+/*   PRE_TAB    field tables of the checksum-only kernel's pre-shifted chains
+ *              (u-domain): F_u = pi o raw(0, chunk), F'_u = pi o Z^4080 o raw(0, chunk) */
+#define ISAL_HIP_CRC64_PRE_TAB (ISAL_HIP_CRC64_SLICE_TAB + ISAL_HIP_CRC64_SLICE_ENTRIES)
+#define ISAL_HIP_CRC64_TAB_ENTRIES (ISAL_HIP_CRC64_PRE_TAB + 2 * ISAL_HIP_CRC64_CHUNK_ENTRIES)
 
 typedef struct {
         long long nfull;      /* full 4 KiB tiles */

@@ -43,6 +43,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_CRC64_FUSED_NV] = {"ISAL_HIP_CRC64_FUSED_NV", NULL},
         [ISAL_HIP_KNOB_CRC_BYTE_DWORDS] = {"ISAL_HIP_CRC_BYTE_DWORDS", NULL},
         [ISAL_HIP_KNOB_CRC_FUSED_NV] = {"ISAL_HIP_CRC_FUSED_NV", NULL},
+        [ISAL_HIP_KNOB_CRC_PRE] = {"ISAL_HIP_CRC_PRE", NULL},
         [ISAL_HIP_KNOB_FAULT] = {"ISAL_HIP_FAULT", NULL},
 };
 

@@ -967,7 +967,8 @@ batch_crc_setup(isal_hip_batch *b)
 {
         uint32_t *h;
         size_t tab = ISAL_HIP_CRC_TAB_DWORDS,
-               plan = ISAL_HIP_CRC_PLAN_DWORDS + ISAL_HIP_CRC_EXT_DWORDS + ISAL_HIP_CRC_B16_DWORDS,
+               plan = ISAL_HIP_CRC_PLAN_DWORDS + ISAL_HIP_CRC_EXT_DWORDS + ISAL_HIP_CRC_B16_DWORDS +
+                      ISAL_HIP_CRC_FPRE_DWORDS,
                nsh, part, tail;
         hipError_t e;
         if (b->d_crc)
@@ -983,6 +984,7 @@ batch_crc_setup(isal_hip_batch *b)
         isal_hip_crc32c_plan(b->len, b->crc.tt, h + tab);
         isal_hip_crc32c_ext_tables(h, h + ISAL_HIP_CRC_EXT_TAB);
         isal_hip_crc32c_byte_tables(h + ISAL_HIP_CRC_B16_TAB);
+        isal_hip_crc32c_pre_tables(h, h + ISAL_HIP_CRC_FPRE_TAB);
         e = hipMalloc((void **) &b->d_crc, (tab + plan) * 4);
         if (e == hipSuccess)
                 e = hipMemcpy(b->d_crc, h, (tab + plan) * 4, hipMemcpyHostToDevice);

@@ -534,6 +534,7 @@ def test_crc_chain_step(engine, oracle, gpu, monkeypatch, step, k, rows, n, ns, 
     count is not a multiple of the load batch."""
     import torch
 
+    _setenv(monkeypatch, "ISAL_HIP_CRC_PRE", "0")  # the chain-step kernel (pre-shifted is the default)
     _setenv(monkeypatch, "ISAL_HIP_CRC_STEP", str(step))
     if tt:
         _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
@@ -780,6 +781,7 @@ def test_crc64_chain_step(engine, oracle, gpu, monkeypatch, step, batch, k, rows
     a multiple of the step."""
     import torch
 
+    _setenv(monkeypatch, "ISAL_HIP_CRC_PRE", "0")  # the chain-step kernel (pre-shifted is the default)
     _setenv(monkeypatch, "ISAL_HIP_CRC64_STEP", str(step))
     _setenv(monkeypatch, "ISAL_HIP_CRC64_BATCH", str(batch))
     if tt:

@@ -107,6 +107,18 @@ for s in $STEPS; do
                         done
                 done
                 ;;
+        prestand)
+                # checksum-only kernels: pre-shifted chains vs chain-step kernels
+                run pytest_gpu_crc 700 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
+                for pre in 0 1; do
+                        for wl in crc crc64; do
+                                ISAL_HIP_CRC_PRE=$pre run bench_${wl}_pre$pre 300 python bench.py --workload $wl --no-cpu-baseline
+                        done
+                done
+                for wl in crc crc64; do
+                        run pmc_lds_${wl}_pre 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_${wl}_pre" -o l -- python3 bench.py --workload $wl --no-cpu-baseline --steps 2 --warmup 1
+                done
+                ;;
         memprobe)
                 # memory-only kernels with the encode addressing: C2 (10 read + 4 write) and C3 decode (10 + 3)
                 run probe_c2 300 isa-l_amd/build/ec_probe 10 4 1048576 1024 5
