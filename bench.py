@@ -649,7 +649,7 @@ def main(argv=None):
                 # lane groups per workgroup: the launcher's rule (crc_kernels.hip fused_nv32)
                 tabs_b, la_b, cap = 32 * 256 * 4, k * 256 * 4, 160 * 1024
                 nv_env = os.environ.get("ISAL_HIP_CRC_FUSED_NV")
-                if not nb or tabs_b + 2 * la_b > cap:
+                if not nb or tabs_b + 2 * la_b >= cap:
                     nv = 1
                 elif nv_env in ("1", "2"):
                     nv = int(nv_env)
@@ -674,7 +674,7 @@ def main(argv=None):
             # lane groups per workgroup: the launcher's rule (crc64_kernels.hip fused_nv)
             tabs_b, la_b, cap = (4992 if sl else 2688) * 8, k * 256 * 8, 160 * 1024
             nv_env = os.environ.get("ISAL_HIP_CRC64_FUSED_NV")
-            if reg or tabs_b + 2 * la_b > cap:
+            if reg or tabs_b + 2 * la_b >= cap:
                 nv = 1
             elif nv_env in ("1", "2"):
                 nv = int(nv_env)

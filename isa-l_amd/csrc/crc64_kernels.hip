@@ -708,7 +708,7 @@ int fused_nv(bool sl, int k) {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_FUSED_NV);
   const size_t cap = 160 * 1024, tabs = (sl ? kSlLds : kKernTab + kCE + kOp) * 8,
                la = static_cast<size_t>(k) * kBlock * 8;
-  if (tabs + 2 * la > cap) return 1;
+  if (tabs + 2 * la >= cap) return 1;  // leave LDS headroom: never the whole 160 KiB
   if (v == 1 || v == 2) return static_cast<int>(v);
   return 2 * (cap / (tabs + 2 * la)) > cap / (tabs + la) ? 2 : 1;
 }

@@ -111,7 +111,7 @@ __device__ __forceinline__ uint32_t shift_tile(const uint32_t* lt, uint32_t a) {
 // 16 byte lookups per chunk, each offset one SDWA shift (byte select + << 2),
 // no chain step; the 256-entry tables are not bank-conflict-free (8 entries
 // per bank): VALU issue traded for LDS cycles. LDS: P at 0, P' at 4096 dwords.
-constexpr int kPos = 0, kPosZ = 16 * 256, kPosLds = 32 * 256;
+[[maybe_unused]] constexpr int kPos = 0, kPosZ = 16 * 256, kPosLds = 32 * 256;
 
 __device__ __forceinline__ void byte_offs4(uint32_t w, uint32_t (&o)[4]) {
   const uint32_t two = 2;
@@ -729,7 +729,7 @@ int crc_byte_dwords() {
 int fused_nv32(int k) {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC_FUSED_NV);
   const size_t cap = 160 * 1024, tabs = kPosLds * 4, la = static_cast<size_t>(k) * kBlock * 4;
-  if (tabs + 2 * la > cap) return 1;
+  if (tabs + 2 * la >= cap) return 1;  // leave LDS headroom: never the whole 160 KiB
   if (v == 1 || v == 2) return static_cast<int>(v);
   return 2 * (cap / (tabs + 2 * la)) > cap / (tabs + la) ? 2 : 1;
 }

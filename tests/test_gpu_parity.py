@@ -520,6 +520,7 @@ CRC_SHAPES = [
     (3, 2, 4096 * 3 + 13, 3, 0),      # len % 16 != 0 -> encode + CRC pass
     (5, 5, 20000, 2, 1),              # unaligned shards -> byte-load CRC kernel
     (4, 10, 4096 * 5, 2, 0),          # rows > 8: two fused passes
+    (64, 4, 4096 * 3 + 32, 2, 0),     # k = 64: the largest fused k (most LDS source chains)
     (70, 3, 4096 * 2 + 32, 2, 0),     # k > 64: encode + CRC pass
     (1, 1, 16, 3, 0),
 ]
@@ -813,6 +814,8 @@ ENCODE_CRC64_SHAPES = [
     (3, 2, 4096 * 2 + 13, 2, 0, None, 3), # len % 16 != 0 -> encode, then CRC64
     (5, 2, 3000, 3, 0, None, 6),          # no full tile -> encode, then CRC64
     (4, 3, 4096 * 4, 2, 5, None, 0),      # unaligned shards -> encode, then CRC64
+    (32, 4, 4096 * 5 + 64, 2, 0, None, 1),  # k = 32: the largest fused k (most LDS source chains)
+    (33, 2, 4096 * 2, 2, 0, None, 2),     # k > 32 -> encode, then CRC64
 ]
 
 

@@ -119,6 +119,9 @@ for s in $STEPS; do
                         run pmc_lds_${wl}_pre 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_${wl}_pre" -o l -- python3 bench.py --workload $wl --no-cpu-baseline --steps 2 --warmup 1
                 done
                 ;;
+        smoke)
+                run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+                ;;
         memprobe)
                 # memory-only kernels with the encode addressing: C2 (10 read + 4 write) and C3 decode (10 + 3)
                 run probe_c2 300 isa-l_amd/build/ec_probe 10 4 1048576 1024 5
