@@ -384,24 +384,25 @@ int load_batch() {
 // Source chains live in registers when the k sources form one load group
 // (REG: k == U, e.g. C2's k = 10), else in LDS (lane-private words).
 // ---------------------------------------------------------------------------
-template <int P, int U, class Feed>
+template <int P, int U, bool R0 = false, class Feed>
 __device__ __forceinline__ void mac_feed(uint32_t (&acc)[P][4], const uint4 (&x)[U], int j,
-                                         const uint32_t* __restrict__ tbl, Feed&& feed) {
+                                         const uint32_t* __restrict__ tbl, Feed&& feed, unsigned long long x0src = 0) {
   constexpr int PAIR = P <= 4 ? 2 : 1;
 #pragma unroll
   for (int u = 0; u + PAIR <= U; u += PAIR) {
     if constexpr (PAIR == 2) {
-      mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
+      mac16x2<P, R0>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl,
+                     r0_mask(x0src, j + u), r0_mask(x0src, j + u + 1));
       feed(j + u, x[u]);
       feed(j + u + 1, x[u + 1]);
     } else {
-      mac16<P>(acc, x[u], tbl + (j + u) * P * kTbl);
+      mac16<P, R0>(acc, x[u], tbl + (j + u) * P * kTbl, r0_mask(x0src, j + u));
       feed(j + u, x[u]);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (PAIR == 2 && (U & 1)) {
-    mac16<P>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl);
+    mac16<P, R0>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl, r0_mask(x0src, j + U - 1));
     feed(j + U - 1, x[U - 1]);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -598,7 +599,7 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
         asm volatile("" : "+s"(z));
         with_phase(phase_of(t), [&](auto phc) __attribute__((always_inline)) {
           tile_body(phc, acc, off, [&](auto& feed) __attribute__((always_inline)) {
-            mac_feed<P, U>(acc, x, 0, tbl + z, feed);
+            mac_feed<P, U, X0>(acc, x, 0, tbl + z, feed, x0src);
           });
         });
       }
@@ -614,12 +615,12 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
             for (; j + U <= k; j += U) {
               uint4 x[U];
               load_grp<U>(x, sp, j, off, len);
-              mac_feed<P, U>(acc, x, j, tbl + z, feed);
+              mac_feed<P, U, X0>(acc, x, j, tbl + z, feed, x0src);
             }
             for (; j < k; ++j) {
               uint4 x[1];
               load_grp<1>(x, sp, j, off, len);
-              mac_feed<P, 1>(acc, x, j, tbl + z, feed);
+              mac_feed<P, 1, X0>(acc, x, j, tbl + z, feed, x0src);
             }
           });
         });
@@ -633,7 +634,7 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
         for (int j = 0; j < k; ++j) {
           uint4 x[1];
           load_grp<1>(x, sp, j, off, len);
-          mac_feed<P, 1>(acc, x, j, tbl, none);
+          mac_feed<P, 1, X0>(acc, x, j, tbl, none, x0src);
         }
 #pragma unroll
         for (int l = 0; l < P; ++l)

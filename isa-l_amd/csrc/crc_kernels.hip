@@ -452,24 +452,25 @@ struct SrcFeed {
 
 // acc ^= the U sources x[] (sources j..j+U-1) times their coefficients; each
 // source also feeds its CRC chain.
-template <int P, int U, class Feed>
+template <int P, int U, bool R0 = false, class Feed>
 __device__ __forceinline__ void mac_feed16(uint32_t (&acc)[P][4], const uint4 (&x)[U], int j,
-                                           const uint32_t* __restrict__ tbl, const Feed& feed) {
+                                           const uint32_t* __restrict__ tbl, const Feed& feed, unsigned long long x0src = 0) {
   constexpr int PAIR = P <= 4 ? 2 : 1;
 #pragma unroll
   for (int u = 0; u + PAIR <= U; u += PAIR) {
     if constexpr (PAIR == 2) {
-      mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
+      mac16x2<P, R0>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl,
+                     r0_mask(x0src, j + u), r0_mask(x0src, j + u + 1));
       feed(j + u, x[u]);
       feed(j + u + 1, x[u + 1]);
     } else {
-      mac16<P>(acc, x[u], tbl + (j + u) * P * kTbl);
+      mac16<P, R0>(acc, x[u], tbl + (j + u) * P * kTbl, r0_mask(x0src, j + u));
       feed(j + u, x[u]);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (PAIR == 2 && (U & 1)) {
-    mac16<P>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl);
+    mac16<P, R0>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl, r0_mask(x0src, j + U - 1));
     feed(j + U - 1, x[U - 1]);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -482,34 +483,36 @@ __device__ __forceinline__ void load_group(uint4 (&x)[U], const uint64_t* __rest
   for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
 }
 
-template <int P, int U, int MODE, class Feed>
+template <int P, int U, int MODE, bool R0, class Feed>
 __device__ __forceinline__ void chunk16_crc(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
                                             int j, long long off, const uint32_t* __restrict__ tbl,
-                                            int len, const Feed& feed) {
+                                            int len, const Feed& feed, unsigned long long x0src) {
   uint4 x[U];
   load_group<U, MODE>(x, sp, j, off, len);
-  mac_feed16<P, U>(acc, x, j, tbl, feed);
+  mac_feed16<P, U, R0>(acc, x, j, tbl, feed, x0src);
 }
 
 // REG: k == U, one load group whose chains are indexed at compile time.
-template <int P, class Pol, bool REG, class Feed>
+// R0: row 0 is the 0/1 row x0src (xor_and instead of GF lookups).
+template <int P, class Pol, bool REG, bool R0, class Feed>
 __device__ __forceinline__ void accum16_crc(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
                                             const uint32_t* __restrict__ tbl, int k, long long off,
-                                            int len, const Feed& feed) {
+                                            int len, const Feed& feed, unsigned long long x0src) {
 #pragma unroll
   for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
   if constexpr (REG) {
-    chunk16_crc<P, Pol::U, Pol::LD>(acc, src, 0, off, tbl, len, feed);
+    chunk16_crc<P, Pol::U, Pol::LD, R0>(acc, src, 0, off, tbl, len, feed, x0src);
   } else {
     int j = 0;
-    for (; j + Pol::U <= k; j += Pol::U) chunk16_crc<P, Pol::U, Pol::LD>(acc, src, j, off, tbl, len, feed);
+    for (; j + Pol::U <= k; j += Pol::U)
+      chunk16_crc<P, Pol::U, Pol::LD, R0>(acc, src, j, off, tbl, len, feed, x0src);
     if constexpr (Pol::U == 4) {
       if (j + 2 <= k) {
-        chunk16_crc<P, 2, Pol::LD>(acc, src, j, off, tbl, len, feed);
+        chunk16_crc<P, 2, Pol::LD, R0>(acc, src, j, off, tbl, len, feed, x0src);
         j += 2;
       }
     }
-    for (; j < k; ++j) chunk16_crc<P, 1, Pol::LD>(acc, src, j, off, tbl, len, feed);
+    for (; j < k; ++j) chunk16_crc<P, 1, Pol::LD, R0>(acc, src, j, off, tbl, len, feed, x0src);
   }
 }
 
@@ -615,9 +618,10 @@ __global__ __launch_bounds__(kBlock * NV, (crc_waves<P, Pol::U, REG>())) void ec
         int z = 0;  // opaque zero: see below
         asm volatile("" : "+s"(z));
         with_last(t + 1 == tf, [&](auto lastc) __attribute__((always_inline)) {
-          mac_feed16<P, Pol::U>(acc, x, 0, tbl + z,
-                                SrcFeed<kFull, NB, decltype(lastc)::value>{
-                                    lt, la, ra, tail + shard_s * kBlock, kLa, tid});
+          mac_feed16<P, Pol::U, X0>(acc, x, 0, tbl + z,
+                                    SrcFeed<kFull, NB, decltype(lastc)::value>{
+                                        lt, la, ra, tail + shard_s * kBlock, kLa, tid},
+                                    x0src);
           store_and_chain(lastc, acc, off);
         });
       }
@@ -630,9 +634,10 @@ __global__ __launch_bounds__(kBlock * NV, (crc_waves<P, Pol::U, REG>())) void ec
         int z = 0;
         asm volatile("" : "+s"(z));
         with_last(t + 1 == tf, [&](auto lastc) __attribute__((always_inline)) {
-          accum16_crc<P, Pol, REG>(acc, sp + src0, tbl + z, k, off, len,
-                                   SrcFeed<kFull, NB, decltype(lastc)::value>{
-                                       lt, la, ra, tail + shard_s * kBlock, kLa, tid});
+          accum16_crc<P, Pol, REG, X0>(acc, sp + src0, tbl + z, k, off, len,
+                                       SrcFeed<kFull, NB, decltype(lastc)::value>{
+                                           lt, la, ra, tail + shard_s * kBlock, kLa, tid},
+                                       x0src);
           store_and_chain(lastc, acc, off);
         });
       }
@@ -642,8 +647,8 @@ __global__ __launch_bounds__(kBlock * NV, (crc_waves<P, Pol::U, REG>())) void ec
       uint32_t* trow = tail + shard_s * kBlock;
       if (off + kVec <= len) {
         uint32_t acc[P][4];
-        accum16_crc<P, Pol, REG>(acc, sp + src0, tbl, k, off, len,
-                                 SrcFeed<kRag, NB>{lt, la, ra, trow, kLa, tid});
+        accum16_crc<P, Pol, REG, X0>(acc, sp + src0, tbl, k, off, len,
+                                     SrcFeed<kRag, NB>{lt, la, ra, trow, kLa, tid}, x0src);
 #pragma unroll
         for (int l = 0; l < P; ++l) {
           store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),

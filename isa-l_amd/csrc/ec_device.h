@@ -110,13 +110,33 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU op (gfx950)
 }
 
+// acc ^ (x & m) in one VALU op: the product of x with a 0/1 coefficient
+// (m = ~0 or 0), e.g. row 0 of every RS Vandermonde matrix (all ones).
+__device__ __forceinline__ uint32_t xor_and(uint32_t acc, uint32_t x, uint32_t m) {
+  return __builtin_amdgcn_bitop3_b32(acc, x, m, 0x78);
+}
+
+// Mask of source j for a 0/1 row: bit j of its source set.
+__device__ __forceinline__ uint32_t r0_mask(unsigned long long src, int j) {
+  return (src >> j) & 1ull ? ~0u : 0u;
+}
+
 // acc[l] ^= c[l][j] * x for the P outputs of this pass; t = tables of source j.
-template <int P>
+// R0: output row 0's coefficient is 0/1 (mask m0), so row 0 is x & m0 — one
+// op per dword instead of three v_perm lookups (the fused encode+CRC kernels,
+// which are VALU-bound, take it when row 0 is such a row).
+template <int P, bool R0 = false>
 __device__ __forceinline__ void mac16(uint32_t (&acc)[P][4], const uint4& x,
-                                      const uint32_t* __restrict__ t) {
+                                      const uint32_t* __restrict__ t, uint32_t m0 = 0) {
   const Sel s[4] = {split(x.x), split(x.y), split(x.z), split(x.w)};
+  if constexpr (R0) {
+    acc[0][0] = xor_and(acc[0][0], x.x, m0);
+    acc[0][1] = xor_and(acc[0][1], x.y, m0);
+    acc[0][2] = xor_and(acc[0][2], x.z, m0);
+    acc[0][3] = xor_and(acc[0][3], x.w, m0);
+  }
 #pragma unroll
-  for (int l = 0; l < P; ++l) {
+  for (int l = R0 ? 1 : 0; l < P; ++l) {
     const Coef c = load_coef(t + l * kTbl);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -129,14 +149,21 @@ __device__ __forceinline__ void mac16(uint32_t (&acc)[P][4], const uint4& x,
 
 // Two sources at once: the six lookups of a (dword, output) fold into the
 // accumulator with three 3-input XORs.
-template <int P>
+template <int P, bool R0 = false>
 __device__ __forceinline__ void mac16x2(uint32_t (&acc)[P][4], const uint4& x, const uint4& y,
                                         const uint32_t* __restrict__ tx,
-                                        const uint32_t* __restrict__ ty) {
+                                        const uint32_t* __restrict__ ty, uint32_t mx = 0,
+                                        uint32_t my = 0) {
   const Sel sx[4] = {split(x.x), split(x.y), split(x.z), split(x.w)};
   const Sel sy[4] = {split(y.x), split(y.y), split(y.z), split(y.w)};
+  if constexpr (R0) {
+    acc[0][0] = xor_and(xor_and(acc[0][0], x.x, mx), y.x, my);
+    acc[0][1] = xor_and(xor_and(acc[0][1], x.y, mx), y.y, my);
+    acc[0][2] = xor_and(xor_and(acc[0][2], x.z, mx), y.z, my);
+    acc[0][3] = xor_and(xor_and(acc[0][3], x.w, mx), y.w, my);
+  }
 #pragma unroll
-  for (int l = 0; l < P; ++l) {
+  for (int l = R0 ? 1 : 0; l < P; ++l) {
     const Coef a = load_coef(tx + l * kTbl);
     const Coef b = load_coef(ty + l * kTbl);
 #pragma unroll

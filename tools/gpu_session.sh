@@ -119,6 +119,16 @@ for s in $STEPS; do
                         run pmc_lds_${wl}_pre 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_${wl}_pre" -o l -- python3 bench.py --workload $wl --no-cpu-baseline --steps 2 --warmup 1
                 done
                 ;;
+        abprev)
+                # A/B against the previous build kept at isa-l_amd/lib/prev (same box)
+                run pytest_gpu_crc 700 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
+                for wl in encode-crc encode-crc64; do
+                        for r in 1 2; do
+                                ISAL_HIP_LIB=isa-l_amd/lib/prev/libisal_hip.so run bench_${wl}_prev$r 300 python bench.py --workload $wl --no-cpu-baseline
+                                run bench_${wl}_new$r 300 python bench.py --workload $wl --no-cpu-baseline
+                        done
+                done
+                ;;
         smoke)
                 run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
                 ;;
