@@ -129,6 +129,14 @@ for s in $STEPS; do
                         done
                 done
                 ;;
+        crctt)
+                # checksum-only kernels: tiles per workgroup now that they are memory-side bound
+                for tt in ${TT_LIST:-16 32 64 128}; do
+                        for wl in crc crc64 encode-crc encode-crc64; do
+                                ISAL_HIP_CRC_TILES=$tt run bench_${wl}_tt$tt 300 python bench.py --workload $wl --no-cpu-baseline
+                        done
+                done
+                ;;
         smoke)
                 run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
                 ;;
