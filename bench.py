@@ -10,10 +10,15 @@ One step = one batched launch that encodes all 1024 stripes
 value = (k+p) * shard_bytes * stripes * steps * n_gpus / wall seconds, GiB/s
         (the reference's perf_print byte convention, erasure_code_perf.c:304).
 
-Multi-GPU: one process per GPU (torchrun), stripes partitioned across ranks
-(weak scaling: every rank encodes its own 1024 stripes from its own HBM); RCCL
+Multi-GPU: one process per GPU, stripes partitioned across ranks (weak
+scaling: every rank encodes its own 1024 stripes from its own HBM); RCCL
 carries only the control plane (broadcast of the coefficient matrix, barrier,
-max-reduce of timings). There is no data-path collective.
+max-reduce of timings). There is no data-path collective. Ranks come either
+from torchrun's environment (RANK / WORLD_SIZE / LOCAL_RANK) or, for
+`bench.py --gpus N` started without one, from this script itself: the parent
+starts N rank processes as fresh children before it touches the GPU, relays
+rank 0's JSON line and exits non-zero when any rank fails. Every rank checks
+that the process group has exactly --gpus ranks, each on its own GPU.
 
 Extra JSON fields:
   roofline      dominant kernel's algorithmic bytes per launch / its average
@@ -43,7 +48,10 @@ GIB = float(1 << 30)
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU). Without a torchrun environment and N > 1 this script "
+                         "starts the N rank processes itself; under torchrun it must equal WORLD_SIZE. "
+                         "Default: WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--k", type=int, default=10)
@@ -84,18 +92,28 @@ def parse_args(argv=None):
 # ---------------------------------------------------------------------------
 
 class Dist:
-    def __init__(self, dry: bool, backend: str = "nccl", always: bool = False):
+    def __init__(self, dry: bool, backend: str = "nccl", always: bool = False, want: int | None = None):
         self.rank = int(os.environ.get("RANK", 0))
         self.world = int(os.environ.get("WORLD_SIZE", 1))
         self.local_rank = int(os.environ.get("LOCAL_RANK", 0))
+        if want is not None and want != self.world:
+            raise SystemExit(f"bench.py: --gpus {want} but this launch has WORLD_SIZE={self.world}")
         self.gpu = self.local_rank
         self.dist = None
         self.backend = None
+        self.shared_gpu = False
         if not dry:
             import torch
 
-            # one process per GPU; ranks beyond the device count (gloo tests) share
-            self.gpu = self.local_rank % max(1, torch.cuda.device_count())
+            # one process per GPU (device_count() does not initialise HIP here).
+            # Only the gloo test mode may put several ranks on one GPU.
+            ndev = max(1, torch.cuda.device_count())
+            if self.local_rank >= ndev:
+                if backend != "gloo":
+                    raise SystemExit(f"bench.py: local rank {self.local_rank} has no GPU of its own "
+                                     f"({ndev} visible); one rank per GPU")
+                self.shared_gpu = True
+            self.gpu = self.local_rank % ndev
         if self.world > 1 or always:
             import torch.distributed as dist
 
@@ -114,6 +132,37 @@ class Dist:
                 torch.cuda.set_device(self.gpu)
                 dist.init_process_group(self.backend, device_id=torch.device("cuda", self.gpu))
             self.dist = dist
+            if dist.get_world_size() != self.world or dist.get_rank() != self.rank:
+                raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks "
+                                 f"(this is {dist.get_rank()}), launch said {self.world} ({self.rank})")
+
+    def topology(self, dry: bool):
+        """Every rank's (GPU index, PCI domain:bus:device) gathered over the
+        control plane; with nccl (RCCL) each rank must sit on a distinct GPU."""
+        if dry:
+            ident = [self.gpu, -1]
+        else:
+            import torch
+
+            pr = torch.cuda.get_device_properties(self.gpu)
+            ident = [self.gpu, (pr.pci_domain_id << 16) | (pr.pci_bus_id << 8) | pr.pci_device_id]
+        flat = [0] * (2 * self.world)
+        flat[2 * self.rank], flat[2 * self.rank + 1] = ident[0] + 1, ident[1] + 1
+        red = self.sum_i64(flat)
+        self.devs = devs = [{"rank": r, "gpu": red[2 * r] - 1,
+                 "pci": None if red[2 * r + 1] <= 0 else "%04x:%02x:%02x" % (
+                     (red[2 * r + 1] - 1) >> 16, ((red[2 * r + 1] - 1) >> 8) & 0xFF, (red[2 * r + 1] - 1) & 0xFF)}
+                for r in range(self.world)]
+        if not dry and self.backend != "gloo":
+            seen = [(x["gpu"], x["pci"]) for x in devs]
+            if len(set(seen)) != len(seen):
+                raise SystemExit(f"bench.py: two ranks share a GPU: {devs}")
+        return devs
+
+    def info(self):
+        return {"dist_backend": self.backend or "none",
+                "rccl_world_size": self.dist.get_world_size() if self.dist and self.backend == "nccl" else None,
+                "rank_devices": self.devs}
 
     def _dev(self):
         import torch
@@ -501,16 +550,19 @@ def total_stripes_run(args, d: Dist, a, k, p, n):
 
     # self-check (all-ones Vandermonde row) and a digest of this rank's shards:
     # CRC32C of every source and parity shard of the resident batch, summed
-    ok = True
-    for s_ in sorted({0, B // 2, B - 1}):
-        x = data[s_, 0].clone()
-        for j in range(1, k):
-            x ^= data[s_, j]
-        ok &= bool(torch.equal(x, out[s_, 0]))
-    crc = torch.zeros(B * (k + p), dtype=torch.int32, device=dev)
-    batch.crc(0xFFFFFFFF, crc, h)
-    torch.cuda.synchronize(dev)
-    digest = int((crc.to(torch.int64) & 0xFFFFFFFF).sum().item())
+    # (a rank whose range is empty — fewer stripes than ranks — encoded nothing
+    # and has nothing to check or digest)
+    ok, digest = True, 0
+    if count:
+        for s_ in sorted({0, B // 2, B - 1}):
+            x = data[s_, 0].clone()
+            for j in range(1, k):
+                x ^= data[s_, j]
+            ok &= bool(torch.equal(x, out[s_, 0]))
+        crc = torch.zeros(B * (k + p), dtype=torch.int32, device=dev)
+        batch.crc(0xFFFFFFFF, crc, h)
+        torch.cuda.synchronize(dev)
+        digest = int((crc.to(torch.int64) & 0xFFFFFFFF).sum().item())
     ranges = [0] * (2 * W)
     ranges[2 * d.rank], ranges[2 * d.rank + 1] = first, count
     red = d.sum_i64([count * args.steps, digest, 0 if ok else 1] + ranges)
@@ -558,6 +610,7 @@ def total_stripes_run(args, d: Dist, a, k, p, n):
             "bytes_per_launch": int(bytes_per_launch),
         },
         "cpu_baseline": None,
+        **d.info(),
     }
     if d.rank == 0:
         print(json.dumps(result), flush=True)
@@ -572,9 +625,85 @@ def total_stripes_run(args, d: Dist, a, k, p, n):
 # main
 # ---------------------------------------------------------------------------
 
+def launch_ranks(args, argv) -> int:
+    """`bench.py --gpus N` (N > 1) with no torchrun environment: start the N
+    rank processes ourselves, one per GPU, as fresh children (this process has
+    not touched the GPU and never execs). Each child gets RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* as torchrun would set them and re-checks them against
+    --gpus. Rank 0's stdout (its JSON line) is relayed to ours, other ranks'
+    stdout goes to stderr. When a rank fails the others would wait in a
+    collective forever, so they are stopped; the exit code is non-zero then."""
+    import signal
+    import socket
+    import subprocess
+
+    n = args.gpus
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs, relays = [], []
+
+    def relay(pipe, out):
+        for line in pipe:
+            out.write(line)
+            out.flush()
+
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                             stdout=subprocess.PIPE, text=True)
+        t = threading.Thread(target=relay, args=(p.stdout, sys.stdout if r == 0 else sys.stderr), daemon=True)
+        t.start()
+        procs.append(p)
+        relays.append(t)
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    old = {sig: signal.signal(sig, lambda *a: (stop(), sys.exit(143))) for sig in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        while True:
+            rcs = [p.poll() for p in procs]
+            if all(rc is not None for rc in rcs):
+                break
+            if any(rc not in (None, 0) for rc in rcs):
+                time.sleep(2)  # let the failing rank's peers report their own error first
+                stop()
+                rcs = [p.poll() for p in procs]
+                break
+            time.sleep(0.1)
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
+    for t in relays:
+        t.join(timeout=5)
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        print(f"bench.py: rank(s) failed (rank, exit code): {bad}", file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse_args(argv)
-    d = Dist(args.dry_run, args.dist_backend, args.dist_always)
+    if args.gpus is not None and args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if (args.gpus or 1) > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
+    d = Dist(args.dry_run, args.dist_backend, args.dist_always, args.gpus)
+    d.topology(args.dry_run)
     if args.dry_run:
         return dry_run(args, d)
 
@@ -833,6 +962,7 @@ def main(argv=None):
             "launch_ms": round(launch_s * 1e3, 4),
             "bytes_per_launch": bytes_per_launch,
         },
+        **d.info(),
     }
     traffic = pmc_traffic(args.workload, k, p, n, S, kernel)
     if traffic:
@@ -932,6 +1062,7 @@ def e2e(args, d: Dist, a, k, p, n):
                  "peak_gb_s_per_direction": 63.0},
         "parity_check_last_stripe": ok,
         "cpu_baseline": None,
+        **d.info(),
     }
     if d.rank == 0:
         print(json.dumps(result), flush=True)
@@ -948,12 +1079,18 @@ def dry_run(args, d: Dist):
     import numpy as np
 
     k, p = args.k, args.p
+    if os.environ.get("ISAL_BENCH_DRY_FAIL_RANK") == str(d.rank):
+        # harness test hook: this rank dies before the first collective, so the
+        # launcher must stop its peers (blocked in the broadcast) and fail
+        raise SystemExit(f"bench.py: dry-run rank {d.rank} failing on request")
     a = control_plane_matrix(d, k, p) if d.rank == 0 or d.world > 1 else b""
     sleep = 0.002 * (1 + d.rank)
     wall = timed_steps(d, lambda: time.sleep(sleep), lambda: None, args.steps, args.warmup)
     total_stripes = d.sum(float(args.stripes))
     out = {"metric": METRIC, "dry_run": True, "n_gpus": d.world, "wall": wall, "stripes": total_stripes,
-           "matrix_fnv": int(np.frombuffer(a, np.uint8).sum())}
+           "matrix_fnv": int(np.frombuffer(a, np.uint8).sum()),
+           "stripe_ranges": [[r * args.stripes, (r + 1) * args.stripes] for r in range(d.world)],
+           **d.info()}
     if args.total_stripes:
         import isal_amd
 

@@ -10,13 +10,22 @@
  *   - every call is synchronous; buffers are owned by the caller; any len >= 0
  *     and any byte alignment is accepted; bytes outside [ptr, ptr+len) are
  *     never touched;
- *   - data-path calls return void and add no failure mode. A GPU runtime error
- *     is reported on stderr and aborts the process (the engine has no silent
- *     CPU fallback).
+ *   - data-path calls return void and add no failure mode (the reference API
+ *     has no error channel; erasure_code.h:108-110 of the reference).
  * Differences: shard buffers may live in host memory OR in device memory
- * (hipMalloc / hipMallocManaged); the engine classifies each pointer and
- * stages host buffers through HBM. The *_base data-path entry points run on
- * the same GPU kernels (their outputs are identical by construction).
+ * (hipMalloc / hipMallocManaged); the engine classifies each pointer
+ * (hipPointerGetAttributes) and routes the call (isal_hip.h, "routing"):
+ *   - any shard in device memory: GPU kernels;
+ *   - all shards in host memory and (k + rows) * len <= 8 MiB: the engine's
+ *     CPU route (ec_cpu.c: AVX-512 GFNI affine, else AVX2 nibble shuffles,
+ *     else per byte) — below that size the GPU round trip costs more;
+ *   - larger host calls: GPU kernels through pinned / HBM staging.
+ * A GPU runtime error during a host-resident call is reported once on stderr
+ * and the columns not yet final finish on the CPU route, so results are
+ * unchanged. A call with any device-resident shard (which no CPU route can
+ * read), or any call under ISAL_HIP_BACKEND=gpu, aborts on a GPU error instead.
+ * The *_base data-path entry points are routed the same way (their outputs
+ * are identical by construction).
  */
 #ifndef ISAL_HIP_ERASURE_CODE_H
 #define ISAL_HIP_ERASURE_CODE_H

@@ -148,6 +148,10 @@ int isal_hip_pipe_destroy(isal_hip_pipe *p);
  * shard is in host memory; data[s*k + j] / coding[s*rows + l] are host
  * pointers (pinned for full copy/compute overlap). Callers whose shards are
  * already in each GPU's HBM use one isal_hip_batch per device instead.
+ * Each device's worker thread runs on the CPUs of the device's NUMA node
+ * (sysfs; ISAL_HIP_SYSFS_ROOT overrides "/sys"), within the process's own
+ * affinity. One handle runs one isal_hip_multi_encode at a time: a second
+ * thread calling it on the same handle blocks until the first returns.
  */
 typedef struct isal_hip_multi isal_hip_multi;
 
@@ -157,6 +161,17 @@ int isal_hip_multi_ndev(const isal_hip_multi *m);
 int isal_hip_multi_encode(isal_hip_multi *m, long long nstripes, unsigned char *const *data,
                           unsigned char *const *coding);
 int isal_hip_multi_destroy(isal_hip_multi *m);
+
+/* NUMA node of device dev's PCIe root (-1 unknown), and how many CPUs its
+ * worker thread is pinned to (0 = not pinned). */
+int isal_hip_multi_numa_node(const isal_hip_multi *m, int dev);
+int isal_hip_multi_worker_cpus(const isal_hip_multi *m, int dev);
+
+/* sysfs lookups behind the pinning (root NULL = ISAL_HIP_SYSFS_ROOT or /sys):
+ * the NUMA node of a PCI device ("0000:05:00.0"; -1 unknown), and the CPUs of
+ * a node's cpulist into cpus[0..max) (returns how many it lists, -1 on error). */
+int isal_hip_pci_numa_node(const char *root, const char *pci_bus_id);
+int isal_hip_numa_node_cpus(const char *root, int node, int *cpus, int max);
 
 /* Stripes [*first, *first + *count) of nstripes belong to device (or rank)
  * dev of ndev: contiguous, covering, sizes differ by at most one. Pure
@@ -176,7 +191,9 @@ void isal_hip_multi_partition(long long nstripes, int ndev, int dev, long long *
  *     host without a usable GPU: the engine's CPU route.
  * ISAL_HIP_BACKEND=gpu forces the kernels for every call (and aborts when no
  * GPU is usable), =cpu sends every host-resident call to the CPU route,
- * =auto (default) is the rule above. If a HIP call fails during a
+ * =auto (default) is the rule above. Routing classifies each shard pointer
+ * with hipPointerGetAttributes, so the HIP runtime is initialised on a host
+ * with a GPU even under =cpu (device-resident shards still go to the GPU). If a HIP call fails during a
  * host-resident call, the call completes on the CPU route and the failure is
  * reported once on stderr; ISAL_HIP_LOG=1 logs every call's route.
  * Environment knobs are read once; isal_hip_config_reload() re-reads them

@@ -4,8 +4,10 @@
  * These are the O(k^2)..O(k^3) control-plane functions that the reference also
  * runs on the host (erasure_code/ec_base.c:37-280): field multiply/inverse,
  * generator matrices, matrix inversion for decode, and table expansion. They
- * never touch shard data. The data path (encode/update/dot/mad/mul) lives in
- * isal_hip_shim.c + ec_kernels.hip and always runs on the GPU.
+ * never touch shard data. The data path (encode/update/dot/mad/mul) is routed
+ * by isal_hip_shim.c: GPU kernels (ec_kernels.hip) for device-resident and
+ * large host-resident calls, the CPU route (ec_cpu.c) for small host calls
+ * and as the fallback of a host call whose GPU attempt failed.
  *
  * Field: GF(2^8) modulo x^8+x^4+x^3+x^2+1 (0x11d). The log/antilog tables are
  * computed once from the polynomial (never copied from ec_base.h).

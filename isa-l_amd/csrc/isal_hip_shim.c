@@ -328,7 +328,11 @@ enum { OP_ENCODE = ISAL_HIP_OP_ENCODE, OP_UPDATE = ISAL_HIP_OP_UPDATE, OP_VERIFY
  * Routes of one synchronous call:
  *   cpu        every shard host-resident and (k + rows) * len <= cpu_max_bytes
  *              (ISAL_HIP_BACKEND=auto), or ISAL_HIP_BACKEND=cpu, or no GPU:
- *              ec_cpu.c, no HIP call at all;
+ *              ec_cpu.c. The routing itself still asks HIP (once per process
+ *              for the device count, then hipPointerGetAttributes per shard
+ *              pointer, ~1 us each), so even ISAL_HIP_BACKEND=cpu initialises
+ *              the HIP runtime when a GPU is present; the arithmetic makes no
+ *              HIP call;
  *   zero-copy  len * (k + rows) <= ZC_BYTES: pointer table, coefficient tables,
  *              host-resident shards and verify slots all live in the pinned
  *              buffer and the kernel reads/writes them over PCIe — the call is
@@ -872,6 +876,7 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         size_t n;
         uint32_t *h;
         hipError_t e;
+        isal_hip_xrows xr;
         if (!b || !gftbls)
                 return ISAL_HIP_EINVAL;
         n = isal_hip_tables_dwords(b->k, b->rows);
@@ -879,7 +884,9 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         if (!h)
                 return ISAL_HIP_ENOMEM;
         isal_hip_build_tables(b->k, b->rows, gftbls, h);
-        isal_hip_xor_rows(b->k, b->rows, gftbls, &b->xr);
+        /* published with the device tables only: a failed update keeps the
+         * old row masks beside the old coefficients */
+        isal_hip_xor_rows(b->k, b->rows, gftbls, &xr);
         if (!b->d_tbl) {
                 if (hipMalloc((void **) &b->d_tbl, n * 4 + 4) != hipSuccess) {
                         free(h);
@@ -894,7 +901,10 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         if (e == hipSuccess)
                 e = hipMemcpy(b->d_tbl, h, n * 4, hipMemcpyHostToDevice);
         free(h);
-        return e == hipSuccess ? ISAL_HIP_OK : ISAL_HIP_EHIP;
+        if (e != hipSuccess)
+                return ISAL_HIP_EHIP;
+        b->xr = xr;
+        return ISAL_HIP_OK;
 }
 
 int
@@ -943,10 +953,11 @@ isal_hip_batch_destroy(isal_hip_batch *b)
 
 /* ---- CRC32C of the batch's shards (isal_hip.h) ---------------------------- */
 
-/* Tiles per CRC workgroup: `def` (CRC32C 16: 64 KiB of each shard, partials
- * 0.4 % of the bytes; CRC64 32: fewer blocks for the combine's Horner steps —
- * C2 sweep, profiles/r02_crc_tile_sweep.txt), halved while the launch would
- * have fewer than 2048 workgroups. ISAL_HIP_CRC_TILES overrides. */
+/* Tiles per CRC workgroup: `def` (CRC32C 64: 256 KiB of each shard per block,
+ * partials 0.1 % of the bytes — profiles/r02_crc_tiles_sweep_b.jsonl; CRC64
+ * 32: fewer blocks for the combine's Horner steps —
+ * profiles/r02_crc_tile_sweep.jsonl), halved while the launch would have
+ * fewer than 2048 workgroups. ISAL_HIP_CRC_TILES overrides. */
 static int
 crc_tiles(int len, int nstripes, int def)
 {

@@ -116,6 +116,10 @@ def lib() -> ctypes.CDLL:
             "isal_hip_multi_destroy": (i, [ctypes.c_void_p]),
             "isal_hip_multi_partition": (None, [ctypes.c_longlong, i, i, ctypes.POINTER(ctypes.c_longlong),
                                                 ctypes.POINTER(ctypes.c_longlong)]),
+            "isal_hip_multi_numa_node": (i, [ctypes.c_void_p, i]),
+            "isal_hip_multi_worker_cpus": (i, [ctypes.c_void_p, i]),
+            "isal_hip_pci_numa_node": (i, [ctypes.c_char_p, ctypes.c_char_p]),
+            "isal_hip_numa_node_cpus": (i, [ctypes.c_char_p, i, ctypes.POINTER(ctypes.c_int), i]),
             "isal_hip_fallbacks": (ctypes.c_ulonglong, []),
             "isal_hip_config_reload": (None, []),
             "isal_hip_max_rows_per_pass": (i, []),
@@ -400,6 +404,14 @@ class Multi:
     def ndev(self) -> int:
         return int(lib().isal_hip_multi_ndev(self._h))
 
+    def numa_node(self, dev: int) -> int:
+        """NUMA node of device dev's PCIe root (-1 unknown)."""
+        return int(lib().isal_hip_multi_numa_node(self._h, dev))
+
+    def worker_cpus(self, dev: int) -> int:
+        """How many CPUs device dev's worker thread is pinned to (0: not pinned)."""
+        return int(lib().isal_hip_multi_worker_cpus(self._h, dev))
+
     def encode(self, nstripes: int, data: Sequence, coding: Sequence) -> None:
         """data[s*k + j], coding[s*rows + l]: host buffers of stripe s."""
         if len(data) != nstripes * self.k or len(coding) != nstripes * self.rows:
@@ -426,6 +438,18 @@ def partition(nstripes: int, ndev: int, dev: int) -> tuple[int, int]:
     first, count = ctypes.c_longlong(), ctypes.c_longlong()
     lib().isal_hip_multi_partition(nstripes, ndev, dev, ctypes.byref(first), ctypes.byref(count))
     return int(first.value), int(count.value)
+
+
+def pci_numa_node(pci_bus_id: str, sysfs_root: str | None = None) -> int:
+    """NUMA node of a PCI device from sysfs (-1 unknown); no GPU needed."""
+    return int(lib().isal_hip_pci_numa_node(sysfs_root.encode() if sysfs_root else None, pci_bus_id.encode()))
+
+
+def numa_node_cpus(node: int, sysfs_root: str | None = None) -> list[int] | None:
+    """CPUs of a NUMA node from its sysfs cpulist (None when unreadable)."""
+    buf = (ctypes.c_int * 4096)()
+    n = lib().isal_hip_numa_node_cpus(sysfs_root.encode() if sysfs_root else None, node, buf, 4096)
+    return None if n < 0 else list(buf[:min(n, 4096)])
 
 
 def kernel_launches() -> int:

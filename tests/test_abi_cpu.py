@@ -123,3 +123,33 @@ def test_raid_argument_contracts_without_gpu(engine):
         assert getattr(L, name)(1, 64, arr) == 1  # vects < 2
     assert L.pq_gen(4, 33, arr) == 1  # len % 32 on the dispatched path
     assert L.pq_gen(4, 0, arr) == 0
+
+
+def test_numa_lookup_against_a_faked_sysfs(engine, tmp_path):
+    """isal_hip_multi pins each device's worker to its NUMA node's CPUs; the
+    lookup (PCI bus id -> numa_node -> cpulist) checked against a fake tree."""
+    root = tmp_path / "sys"
+    dev = root / "bus" / "pci" / "devices" / "0000:c5:00.0"
+    dev.mkdir(parents=True)
+    (dev / "numa_node").write_text("1\n")
+    none = root / "bus" / "pci" / "devices" / "0000:05:00.0"
+    none.mkdir(parents=True)
+    (none / "numa_node").write_text("-1\n")
+    for n, lst in ((0, "0-3,8-11\n"), (1, "4-7,12,14-15\n")):
+        d = root / "devices" / "system" / "node" / f"node{n}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(lst)
+    r = str(root)
+    # bus ids come from hipDeviceGetPCIBusId in upper case; sysfs is lower case
+    assert engine.pci_numa_node("0000:C5:00.0", r) == 1
+    assert engine.pci_numa_node("0000:05:00.0", r) == -1  # no NUMA affinity reported
+    assert engine.pci_numa_node("0000:99:00.0", r) == -1  # no such device
+    assert engine.numa_node_cpus(0, r) == [0, 1, 2, 3, 8, 9, 10, 11]
+    assert engine.numa_node_cpus(1, r) == [4, 5, 6, 7, 12, 14, 15]
+    assert engine.numa_node_cpus(2, r) is None
+    (root / "devices" / "system" / "node" / "node2").mkdir()
+    (root / "devices" / "system" / "node" / "node2" / "cpulist").write_text("3-1\n")
+    assert engine.numa_node_cpus(2, r) is None  # malformed range
+    # the real tree of this host parses (node 0 exists on every Linux box with NUMA)
+    if os.path.exists("/sys/devices/system/node/node0/cpulist"):
+        assert engine.numa_node_cpus(0, None)

@@ -1233,22 +1233,27 @@ def test_bench_two_ranks_on_one_gpu(gpu):
     import socket
     import sys
 
-    sock = socket.socket()
-    sock.bind(("127.0.0.1", 0))
-    port = sock.getsockname()[1]
-    sock.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(ecutil.REPO, "bench.py"), "--dist-backend", "gloo", "--stripes", "64",
-           "--len", "65536", "--steps", "4", "--warmup", "1"]
+    # the driver's own form: `bench.py --gpus 2` with no torchrun, bench.py starts
+    # both ranks itself (gloo lets them share this box's one GPU)
+    env = {a: b for a, b in os.environ.items() if a not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ecutil.REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--stripes", "64", "--len", "65536", "--steps", "4", "--warmup", "1"]
     for workload in ("encode", "decode"):
         r = subprocess.run(cmd + ["--workload", workload], capture_output=True, text=True,
-                           timeout=600, cwd=ecutil.REPO)
+                           timeout=600, cwd=ecutil.REPO, env=env)
         assert r.returncode == 0, r.stderr[-3000:]
         lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
         assert len(lines) == 1, r.stdout
         out = json.loads(lines[0])
         assert out["n_gpus"] == 2 and out["value"] > 0 and out["self_check"] is True, out
+        assert [d["rank"] for d in out["rank_devices"]] == [0, 1] and out["dist_backend"] == "gloo"
+    # under torchrun the same flags must agree with WORLD_SIZE
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] + cmd[1:]
     # C5 mode: 300 stripes split over the two ranks, batches of 64 (4 full + 1 ragged
     # launch per rank), every stripe counted once per step
     r = subprocess.run(cmd + ["--total-stripes", "300"], capture_output=True, text=True, timeout=600,
@@ -1258,6 +1263,46 @@ def test_bench_two_ranks_on_one_gpu(gpu):
     assert out["config"]["stripe_ranges"] == [[0, 150], [150, 300]], out
     assert out["stripes_encoded"] == 300 * 4 and out["self_check"] is True, out
     assert out["scaling"] == "strong" and out["value"] > 0
+
+
+def test_differential_fuzz_on_the_kernels(gpu, tmp_path):
+    """tests/fuzz/ec_diff_fuzz.c against the shipped libisal_hip.so with every
+    call forced onto the kernels: encode / update / dot / mad / mul / RAID
+    gen + check with len in [0, 16384], k and rows up to 16, raw table bytes,
+    misaligned shards, each output and canary compared with the oracle
+    (the reference's own fuzz harness only looks for crashes,
+    tests/fuzz/ec_fuzz_test.c:322-348)."""
+    import sys
+
+    exe = os.path.join(ecutil.ENGINE_DIR, "build", "fuzzgpu", "ec_diff_fuzz_gpu")
+    assert os.path.exists(exe), "build() makes it: make -C tests/fuzz gpu"
+    corpus = tmp_path / "corpus"
+    subprocess.run([sys.executable, os.path.join(ecutil.REPO, "tests", "fuzz", "seeds.py"), "diff", str(corpus)],
+                   check=True, capture_output=True)
+    env = dict(os.environ, ISAL_HIP_BACKEND="gpu")
+    r = subprocess.run([exe, "-max_total_time=45", "-max_len=300000", "-print_final_stats=1",
+                        f"-artifact_prefix={tmp_path}/", str(corpus)],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=tmp_path)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    runs = [int(l.split(":")[-1]) for l in out.splitlines() if l.startswith("stat::number_of_executed_units")]
+    assert runs and runs[0] >= 200, out[-2000:]
+
+
+def test_bench_refuses_more_rccl_ranks_than_gpus(gpu):
+    """`bench.py --gpus N` over RCCL with fewer than N GPUs visible must fail
+    loudly instead of stacking ranks on one GPU (or running one rank)."""
+    import sys
+    import torch
+
+    n = torch.cuda.device_count() + 1
+    env = {a: b for a, b in os.environ.items() if a not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ecutil.REPO, "bench.py"), "--gpus", str(n),
+                        "--stripes", "8", "--len", "65536", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=300, cwd=ecutil.REPO, env=env)
+    assert r.returncode != 0
+    assert "has no GPU of its own" in r.stderr and "rank(s) failed" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
 
 
 def test_bench_rccl_control_plane_single_rank(gpu):
@@ -1284,6 +1329,7 @@ def test_bench_rccl_control_plane_single_rank(gpu):
         out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
         assert out["n_gpus"] == 1 and out["self_check"] is True and out["value"] > 0, out
         assert out["shard_crc32c_digest"] > 0
+        assert out["rccl_world_size"] == 1 and out["rank_devices"][0]["pci"], out
 
 
 def test_multi_device_encode_host_stripes_vs_oracle(engine, oracle, gpu):
@@ -1299,6 +1345,14 @@ def test_multi_device_encode_host_stripes_vs_oracle(engine, oracle, gpu):
     par = torch.full((ns, p, n), 0xEE, dtype=torch.uint8).pin_memory()
     m = engine.Multi(n, k, p, tbls, ndev=0, depth=2)
     assert m.ndev == torch.cuda.device_count()
+    for d in range(m.ndev):
+        # the device's NUMA node from sysfs, and its worker pinned within our affinity
+        bus = torch.cuda.get_device_properties(d)
+        want = engine.pci_numa_node("%04x:%02x:%02x.0" % (bus.pci_domain_id, bus.pci_bus_id, bus.pci_device_id))
+        assert m.numa_node(d) == want
+        assert 0 <= m.worker_cpus(d) <= len(os.sched_getaffinity(0))
+        assert (m.worker_cpus(d) > 0) == (want >= 0 and bool(
+            set(engine.numa_node_cpus(want) or []) & os.sched_getaffinity(0)))
     launches = engine.kernel_launches()
     m.encode(ns, [src[s, j] for s in range(ns) for j in range(k)], [par[s, l] for s in range(ns) for l in range(p)])
     assert engine.kernel_launches() >= launches + ns

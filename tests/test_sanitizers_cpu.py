@@ -50,3 +50,49 @@ def test_reference_test_programs_under_asan_ubsan(sanitized_builds):
         assert v is not None, f"{name} not built"
         rc, out = v
         assert rc == 0 and "pass" in out.lower(), (name, out)
+
+
+# ---------------------------------------------------------------------------
+# libFuzzer (the reference fuzzes init / encode / dot_prod / mad with
+# len in [0, 16384], tests/fuzz/ec_fuzz_test.c). Three targets, each bounded:
+#   ec_fuzz_test, raid_fuzz_test  the reference's own harnesses, unmodified,
+#                                 linked against the engine (crash / ASan /
+#                                 UBSan / leak oracle);
+#   ec_diff_fuzz                  tests/fuzz/ec_diff_fuzz.c: every input through
+#                                 the engine and the oracle, outputs compared.
+# ---------------------------------------------------------------------------
+
+FUZZ_DIR = os.path.join(ecutil.ENGINE_DIR, "build", "fuzz")
+FUZZ_SECONDS = int(os.environ.get("ISAL_FUZZ_SECONDS", "20"))
+# report_globals=0: this toolchain's static link registers some TUs' globals
+# twice (a false odr-violation at start-up); heap, stack and UB checks stay on
+FUZZ_ENV = dict(os.environ, ISAL_HIP_BACKEND="cpu", ASAN_OPTIONS="report_globals=0:detect_leaks=1",
+                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+
+
+@pytest.fixture(scope="module")
+def fuzz_builds():
+    targets = ["all"] + (["ref"] if os.path.isdir("/root/reference/tests/fuzz") else [])
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ecutil.REPO, "tests", "fuzz"), "-j8"] + targets,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("target,layout", [("ec_diff_fuzz", "diff"), ("ec_fuzz_test", "ec"),
+                                           ("raid_fuzz_test", "raid")])
+def test_libfuzzer_targets(fuzz_builds, tmp_path, target, layout):
+    import sys
+
+    exe = os.path.join(FUZZ_DIR, target)
+    if not os.path.exists(exe):
+        pytest.skip(f"{target} not built (the reference's harnesses need /root/reference)")
+    corpus = tmp_path / "corpus"
+    subprocess.run([sys.executable, os.path.join(ecutil.REPO, "tests", "fuzz", "seeds.py"), layout, str(corpus)],
+                   check=True, capture_output=True)
+    r = subprocess.run([exe, f"-max_total_time={FUZZ_SECONDS}", "-max_len=300000", "-print_final_stats=1",
+                        f"-artifact_prefix={tmp_path}/", str(corpus)],
+                       capture_output=True, text=True, timeout=FUZZ_SECONDS + 300, env=FUZZ_ENV, cwd=tmp_path)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    runs = [int(l.split(":")[-1]) for l in out.splitlines() if l.startswith("stat::number_of_executed_units")]
+    assert runs and runs[0] >= 200, out[-2000:]  # the seeds alone are ~150-200 inputs

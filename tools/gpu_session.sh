@@ -33,6 +33,23 @@ for s in $STEPS; do
                 run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread
                 grep -E "PASSED|FAILED|SKIPPED|ERROR|passed|failed" "$OUT/pytest_gpu.log" > "$OUT/pytest_gpu_summary.txt" || true
                 ;;
+        benchtests)
+                run pytest_gpu_bench 600 python -u -m pytest tests -m gpu -x -v -k "bench" --timeout 300 --timeout-method thread
+                ;;
+        stage)
+                # how a synchronous host-resident call can move pageable shards (tools/stage_probe.c)
+                run stage_probe 300 tools/stage_probe
+                ;;
+        fuzzgpu)
+                # differential fuzzing of the shipped library on the kernels (tests/fuzz)
+                python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
+                ISAL_HIP_BACKEND=gpu run fuzz_gpu 200 isa-l_amd/build/fuzzgpu/ec_diff_fuzz_gpu -max_total_time=90 -max_len=300000 -print_final_stats=1 -print_pcs=0 "$OUT/fuzz_corpus"
+                rm -rf "$OUT/fuzz_corpus"
+                ;;
+        gpus2)
+                # the driver's N>1 form on this one-GPU box: two gloo ranks share the GPU
+                run bench_gpus2_gloo 300 python bench.py --gpus 2 --dist-backend gloo --no-cpu-baseline
+                ;;
         tests_crc)
                 run pytest_gpu_crc 300 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
                 ;;
