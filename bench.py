@@ -799,9 +799,13 @@ def main(argv=None):
             bytes_per_launch = (k + p) * n * S
             u = enc_group(k)
             reg = k == u and os.environ.get("ISAL_HIP_CRC64_SRC_CHAIN") == "reg"
-            sl = os.environ.get("ISAL_HIP_CRC64_SLICE") != "0"  # slicing-by-8 chunk path (default)
+            # chunk path: 0 field tables, 1 slicing-by-8 byte tables (default), 2 hybrid
+            # byte/field tables (experiment, load group 10 only)
+            sl = {"0": 0, "2": 2}.get(os.environ.get("ISAL_HIP_CRC64_SLICE", "1"), 1)
+            if sl == 2 and (u != 10 or reg):
+                sl = 1
             # lane groups per workgroup: the launcher's rule (crc64_kernels.hip fused_nv)
-            tabs_b, la_b, cap = (4992 if sl else 2688) * 8, k * 256 * 8, 160 * 1024
+            tabs_b, la_b, cap = {0: 2688, 1: 4096, 2: 1024}[sl] * 8, k * 256 * 8, 160 * 1024
             nv_env = os.environ.get("ISAL_HIP_CRC64_FUSED_NV")
             if reg or tabs_b + 2 * la_b >= cap:
                 nv = 1
@@ -810,7 +814,7 @@ def main(argv=None):
             else:
                 nv = 2 if 2 * (cap // (tabs_b + 2 * la_b)) > cap // (tabs_b + la_b) else 1
             # X0: Vandermonde row 0 derived
-            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(reg).lower()}, true, {str(sl).lower()}, {nv}>"
+            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(reg).lower()}, true, {sl}, {nv}>"
             workload = (f"C2 encode + CRC64 (crc64_ecma_refl) of all k+p shards in one pass: k={k} "
                         f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
         elif args.workload == "crc64":
@@ -985,9 +989,12 @@ def main(argv=None):
                 # the reference's fast x86 path (AVX-512+GFNI, gf_Nvect_dot_prod_avx512_gfni)
                 # restated in C intrinsics: cache-warm like the reference harness, and
                 # cold (each thread cycling over distinct stripes, HBM-like streaming)
+                # encode: the port's parity of stripe 0 is compared with the GPU's
+                # (decode would need the decode matrix, which the port does not take)
+                port_check = (data[0].cpu().numpy(), out[0].cpu().numpy()) if args.workload == "encode" else None
                 for key, ring in (("cpu_baseline_simd_port", 1), ("cpu_baseline_simd_port_cold", args.cold_ring)):
-                    result[key] = cpu_baseline(k, rows, n, min(args.cpu_seconds, 5.0), threads, None,
-                                               impl="gfni", ring=ring)
+                    result[key] = cpu_baseline(k, rows, n, min(args.cpu_seconds, 5.0), threads,
+                                               port_check if ring == 1 else None, impl="gfni", ring=ring)
         else:
             check = None
             if args.workload in ("encode-crc", "encode-crc64"):

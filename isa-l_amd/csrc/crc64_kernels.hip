@@ -460,6 +460,15 @@ __device__ __forceinline__ void byte_offs8(uint32_t w, uint32_t (&o)[4]) {
       : "=v"(o[3]) : "v"(three), "v"(w));
 }
 
+// Bytes 0 and 2 of w times 8.
+__device__ __forceinline__ void byte_offs8(uint32_t w, uint32_t& o0, uint32_t& o2) {
+  const uint32_t three = 3;
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+      : "=v"(o0) : "v"(three), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+      : "=v"(o2) : "v"(three), "v"(w));
+}
+
 __device__ __forceinline__ uint64_t tab8_at(const uint64_t* t, int j, uint32_t o) {
   return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(t) + j * 2048 + o);
 }
@@ -475,15 +484,80 @@ __device__ __forceinline__ void slice8_acc(X64& acc, const uint64_t* t, uint32_t
   acc.add2(tab8_at(t, 6, q[2]), tab8_at(t, 7, q[3]));
 }
 
+// Hybrid tables (SL == 2, an LDS bank-conflict experiment): each byte b_j of
+// the 8-byte word splits into its high 5 bits — a 32-entry table H_j, one bank
+// row, conflict-free, offset (b_j & 0xF8) in one SDWA op — and its low 3 bits,
+// paired with its neighbour's into a 6-bit field of a 64-entry table G_q (two
+// rows, at most 2-way). 12 lookups per 8 bytes instead of 8, LDS 8 KiB
+// instead of 32 KiB; derived in LDS from the byte tables at kernel start
+// (A_j linear: A_j[v] = H_j[v >> 3] ^ A_j[v & 7]).
+constexpr int kHyG = 8 * 32;        // G tables after the 8 H tables (entries)
+constexpr int kHySet = kHyG + 4 * 64;  // one hybrid set (A or A')
+constexpr int kHyLds = 2 * kHySet;
+
+__device__ __forceinline__ void hybrid_tables(uint64_t* lt, const uint64_t* __restrict__ bytes,
+                                              int nthreads) {
+  for (int i = threadIdx.x; i < kHyLds; i += nthreads) {
+    const int set = i / kHySet, r = i % kHySet;
+    const uint64_t* a = bytes + set * (8 * 256);
+    uint64_t v;
+    if (r < kHyG) {
+      v = a[(r / 32) * 256 + ((r % 32) << 3)];
+    } else {
+      const int q = (r - kHyG) / 64, f = (r - kHyG) % 64;
+      v = a[(2 * q) * 256 + (f & 7)] ^ a[(2 * q + 1) * 256 + (f >> 3)];
+    }
+    lt[i] = v;
+  }
+}
+
+// acc ^= S(w) for one dword (bytes j0..j0+3 of the 8-byte word) through the
+// hybrid set at t: 4 H lookups + 2 G lookups, 9 VALU offset ops.
+template <int J0>
+__device__ __forceinline__ void hyb4_acc(X64& acc, const uint64_t* t, uint32_t w) {
+  const uint32_t m = 0xF8u;
+  uint32_t h[4];
+  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+      : "=v"(h[0]) : "v"(m), "v"(w));
+  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+      : "=v"(h[1]) : "v"(m), "v"(w));
+  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+      : "=v"(h[2]) : "v"(m), "v"(w));
+  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+      : "=v"(h[3]) : "v"(m), "v"(w));
+  // f byte 0 = lo3(b0) | lo3(b1) << 3, f byte 2 = lo3(b2) | lo3(b3) << 3
+  const uint32_t f = ((w >> 5) & 0x00380038u) | (w & 0x07070707u);
+  uint32_t g[2];
+  byte_offs8(f, g[0], g[1]);
+  const char* tc = reinterpret_cast<const char*>(t);
+  auto H = [&](int j, uint32_t o) { return *reinterpret_cast<const uint64_t*>(tc + (J0 + j) * 256 + o); };
+  auto G = [&](int q, uint32_t o) {
+    return *reinterpret_cast<const uint64_t*>(tc + kHyG * 8 + (J0 / 2 + q) * 512 + o);
+  };
+  acc.add2(H(0, h[0]), H(1, h[1]));
+  acc.add2(H(2, h[2]), H(3, h[3]));
+  acc.add2(G(0, g[0]), G(1, g[1]));
+}
+
+__device__ __forceinline__ void hyb8_acc(X64& acc, const uint64_t* t, uint32_t lo, uint32_t hi) {
+  hyb4_acc<0>(acc, t, lo);
+  hyb4_acc<4>(acc, t, hi);
+}
+
 // One tile of a pre-shifted u-domain chain b (phase 1: the block's last tile,
-// which returns the plain chain a instead).
-template <int PH>
+// which returns the plain chain a instead). SL 1: byte tables, 2: hybrid.
+template <int PH, int SL = 1>
 __device__ __forceinline__ uint64_t chain_step_sl(const uint64_t* lt, uint64_t b, uint32_t w0,
                                                   uint32_t w1, uint32_t w2, uint32_t w3) {
   X64 u{0u, 0u};
-  slice8_acc(u, lt + kSA, w0 ^ static_cast<uint32_t>(b), w1 ^ static_cast<uint32_t>(b >> 32));
   X64 c{0u, 0u};
-  slice8_acc(c, lt + (PH == 1 ? kSA : kSB), w2 ^ u.lo, w3 ^ u.hi);
+  if constexpr (SL == 2) {
+    hyb8_acc(u, lt, w0 ^ static_cast<uint32_t>(b), w1 ^ static_cast<uint32_t>(b >> 32));
+    hyb8_acc(c, lt + (PH == 1 ? 0 : kHySet), w2 ^ u.lo, w3 ^ u.hi);
+  } else {
+    slice8_acc(u, lt + kSA, w0 ^ static_cast<uint32_t>(b), w1 ^ static_cast<uint32_t>(b >> 32));
+    slice8_acc(c, lt + (PH == 1 ? kSA : kSB), w2 ^ u.lo, w3 ^ u.hi);
+  }
   return c.get();
 }
 
@@ -504,15 +578,17 @@ constexpr int fused64_waves() {
 // NV: independent 256-lane groups per workgroup. They share one LDS copy of the
 // tables (each works its own items, no barrier after the table load), so the
 // per-lane source chains, not the tables, set how many waves fit a CU.
-template <int P, int U, bool REG, bool X0 = false, bool SL = false, int NV = 1>
+template <int P, int U, bool REG, bool X0 = false, int SL = 0, int NV = 1>
 __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_encode_crc64_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, const uint32_t* __restrict__ tbl, int len,
     int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged, int pair,
     unsigned long long x0src, int uswap, const uint64_t* __restrict__ tabs,
     uint64_t* __restrict__ part) {
-  __shared__ uint64_t lt[SL ? kSlLds : kKernTab + kCE + kOp];
+  __shared__ uint64_t lt[SL == 2 ? kHyLds : SL ? kSlLds : kKernTab + kCE + kOp];
   extern __shared__ uint64_t la[];  // [k][kBlock * NV] source chains when !REG
-  if constexpr (SL) {
+  if constexpr (SL == 2) {
+    hybrid_tables(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB, kBlock * NV);
+  } else if constexpr (SL) {
     load_lds<kSlLds, NV>(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB);
   } else {
     load_lds<kKernTab, NV>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
@@ -525,7 +601,7 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
   auto step = [&](auto phc, uint64_t a, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
                   __attribute__((always_inline)) {
     if constexpr (SL)
-      return chain_step_sl<decltype(phc)::value>(lt, a, w0, w1, w2, w3);
+      return chain_step_sl<decltype(phc)::value, SL>(lt, a, w0, w1, w2, w3);
     else
       return chain_step<decltype(phc)::value>(lt, a, w0, w1, w2, w3);
   };
@@ -697,17 +773,20 @@ bool src_chain_reg64() {
 // (ISAL_HIP_CRC64_SLICE=0 selects the field tables). C2 step, LDS chains, two
 // lane groups: 4.58 -> 4.01 ms (VALU 2.40e9 -> 1.83e9 wave-instructions,
 // profiles/r02_fastcrc_*); with register chains (240 VGPRs) it is slower.
-bool slice64() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_SLICE) != 0;
+// 0: field tables, 1: byte (slicing) tables, 2: hybrid tables (experiment,
+// instantiated for the C2 load group U = 10 only; other U use byte tables).
+int slice64() {
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_SLICE);
+  return v == 0 ? 0 : v == 2 ? 2 : 1;
 }
 
 // 256-lane groups per workgroup of the LDS-chain fused kernel: the knob
 // (ISAL_HIP_CRC64_FUSED_NV = 1 or 2) or, unset, 2 when that fits more lane
 // groups on a CU (160 KiB of LDS; the static tables are shared by a workgroup,
 // the source chains are per lane).
-int fused_nv(bool sl, int k) {
+int fused_nv(int sl, int k) {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_FUSED_NV);
-  const size_t cap = 160 * 1024, tabs = (sl ? kSlLds : kKernTab + kCE + kOp) * 8,
+  const size_t cap = 160 * 1024, tabs = (sl == 2 ? kHyLds : sl ? kSlLds : kKernTab + kCE + kOp) * 8,
                la = static_cast<size_t>(k) * kBlock * 8;
   if (tabs + 2 * la >= cap) return 1;  // leave LDS headroom: never the whole 160 KiB
   if (v == 1 || v == 2) return static_cast<int>(v);
@@ -731,13 +810,19 @@ void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_
   } while (0)
   const size_t lds = static_cast<size_t>(k) * kBlock * 8;
   const bool reg = k == U && src_chain_reg64();
-  const bool sl = slice64(), nv2 = !reg && fused_nv(sl, k) == 2;
+  int sl = slice64();
+  if (sl == 2 && (U != 10 || reg)) sl = 1;
+  const bool nv2 = !reg && fused_nv(sl, k) == 2;
   if (reg) {
-    if (sl) FUSED64_X0(true, true, 1); else FUSED64_X0(true, false, 1);
+    if (sl) FUSED64_X0(true, 1, 1); else FUSED64_X0(true, 0, 1);
+  } else if (sl == 2) {
+    if constexpr (U == 10) {
+      if (nv2) FUSED64_X0(false, 2, 2); else FUSED64_X0(false, 2, 1);
+    }
   } else if (sl) {
-    if (nv2) FUSED64_X0(false, true, 2); else FUSED64_X0(false, true, 1);
+    if (nv2) FUSED64_X0(false, 1, 2); else FUSED64_X0(false, 1, 1);
   } else {
-    if (nv2) FUSED64_X0(false, false, 2); else FUSED64_X0(false, false, 1);
+    if (nv2) FUSED64_X0(false, 0, 2); else FUSED64_X0(false, 0, 1);
   }
 #undef FUSED64_X0
 #undef FUSED64_LAUNCH

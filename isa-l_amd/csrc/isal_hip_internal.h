@@ -110,6 +110,9 @@ enum {
         ISAL_HIP_KNOB_CRC_FUSED_NV,    /* 256-lane groups per fused encode+CRC32C workgroup: 1 | 2 */
         ISAL_HIP_KNOB_CRC_PRE,         /* checksum-only CRC32C/CRC64 kernels: pre-shifted chains (default) | 0 */
         ISAL_HIP_KNOB_FAULT,           /* fault-injection site of GPU-routed calls (tests) */
+        ISAL_HIP_KNOB_FAULT_CHUNK,     /* ... only in this column chunk of a call (tests; unset: every chunk) */
+        ISAL_HIP_KNOB_CHUNK_KB,        /* column-chunk bytes per shard of large host calls (pipelined) */
+        ISAL_HIP_KNOB_PIPE_CHUNKS,     /* 0: large host calls one chunk at a time (no copy overlap) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

@@ -45,6 +45,9 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_CRC_FUSED_NV] = {"ISAL_HIP_CRC_FUSED_NV", NULL},
         [ISAL_HIP_KNOB_CRC_PRE] = {"ISAL_HIP_CRC_PRE", NULL},
         [ISAL_HIP_KNOB_FAULT] = {"ISAL_HIP_FAULT", NULL},
+        [ISAL_HIP_KNOB_FAULT_CHUNK] = {"ISAL_HIP_FAULT_CHUNK", NULL},
+        [ISAL_HIP_KNOB_CHUNK_KB] = {"ISAL_HIP_CHUNK_KB", NULL},
+        [ISAL_HIP_KNOB_PIPE_CHUNKS] = {"ISAL_HIP_PIPE_CHUNKS", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];

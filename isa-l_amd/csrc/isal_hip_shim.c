@@ -167,6 +167,12 @@ gpu_present(void)
 /* Host-resident shards are staged through HBM in chunks of at most this many
  * bytes in total (override: ISAL_HIP_STAGE_MB). */
 #define DEFAULT_STAGE_BYTES (256u << 20)
+/* Large host calls are cut into column chunks of this many bytes per shard
+ * (override: ISAL_HIP_CHUNK_KB) that flow through PIPE_NBUF staging buffers:
+ * the H2D copy of chunk i+1, the kernel of chunk i and the D2H copy of chunk
+ * i-1 run at once on three streams. */
+#define DEFAULT_CHUNK_BYTES ((size_t) 1 << 20)
+#define PIPE_NBUF 3
 
 typedef struct {
         int device;
@@ -177,7 +183,38 @@ typedef struct {
         size_t args_cap;
         unsigned char *d_stage; /* device scratch for host-resident shards */
         size_t stage_cap;
+        /* pipelined column chunks (gpu_pipelined): copy-in / copy-out streams
+         * and per-buffer events, created on first use */
+        hipStream_t s_in, s_out;
+        hipEvent_t ev_in[PIPE_NBUF], ev_k[PIPE_NBUF], ev_out[PIPE_NBUF];
+        int pipe_ready;
+        struct outq *oq; /* the call thread's copy-out worker (gpu_pipelined) */
 } ctx_t;
+
+/* Copy-out worker of a calling thread. The runtime serves a copy from or to
+ * pageable memory synchronously on the thread that issues it (tools/
+ * stage_probe.c: hipMemcpyAsync returns when the copy is done), so copies in
+ * and out overlap only when two host threads issue them: the calling thread
+ * stages chunks in and launches, this worker copies chunks out in order. */
+typedef struct outq {
+        pthread_t th;
+        pthread_mutex_t mu;
+        pthread_cond_t cv;
+        int quit, active;
+        long long posted, handled; /* chunks launched / whose output copies are enqueued */
+        /* the call being served */
+        int op, nsrc, nptr, len;
+        const int *flag;
+        unsigned char *const *dst;
+        size_t chunk, slot, set_bytes;
+        /* the worker's first failure */
+        hipError_t err;
+        const char *what;
+        long long fail_chunk;
+        int rows_out;
+} outq_t;
+
+static void outq_stop(ctx_t *c);
 
 static pthread_key_t ctx_key;
 static pthread_once_t ctx_once = PTHREAD_ONCE_INIT;
@@ -197,6 +234,18 @@ ctx_release(void *p)
                 (void) hipHostFree(c->h_args);
         if (c->d_stage)
                 (void) hipFree(c->d_stage);
+        if (c->oq)
+                outq_stop(c);
+        if (c->pipe_ready) {
+                int b;
+                (void) hipStreamDestroy(c->s_in);
+                (void) hipStreamDestroy(c->s_out);
+                for (b = 0; b < PIPE_NBUF; b++) {
+                        (void) hipEventDestroy(c->ev_in[b]);
+                        (void) hipEventDestroy(c->ev_k[b]);
+                        (void) hipEventDestroy(c->ev_out[b]);
+                }
+        }
         free(c);
 }
 
@@ -292,6 +341,34 @@ ensure_stage(ctx_t *c, size_t bytes)
         if ((e = hipMalloc((void **) &c->d_stage, bytes)) != hipSuccess)
                 return e;
         c->stage_cap = bytes;
+        return hipSuccess;
+}
+
+static hipError_t
+ensure_pipe(ctx_t *c)
+{
+        hipError_t e;
+        int b;
+        if (c->pipe_ready)
+                return hipSuccess;
+        if ((e = hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking)) != hipSuccess)
+                return e;
+        if ((e = hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking)) != hipSuccess) {
+                (void) hipStreamDestroy(c->s_in);
+                return e;
+        }
+        for (b = 0; b < PIPE_NBUF; b++) {
+                if ((e = hipEventCreateWithFlags(&c->ev_in[b], hipEventDisableTiming)) != hipSuccess ||
+                    (e = hipEventCreateWithFlags(&c->ev_k[b], hipEventDisableTiming)) != hipSuccess ||
+                    (e = hipEventCreateWithFlags(&c->ev_out[b], hipEventDisableTiming)) != hipSuccess) {
+                        /* leak the few created events: this only happens when the
+                         * runtime is failing anyway */
+                        (void) hipStreamDestroy(c->s_in);
+                        (void) hipStreamDestroy(c->s_out);
+                        return e;
+                }
+        }
+        c->pipe_ready = 1;
         return hipSuccess;
 }
 
@@ -422,21 +499,27 @@ enum {
         FAULT_SYNC = 5,   /* the final stream synchronisation */
 };
 
+/* ISAL_HIP_FAULT_CHUNK=n narrows the fault to column chunk n of a call, so
+ * the fallback also runs after earlier chunks finished on the GPU. */
 static int
-fault_at(int site)
+fault_at(int site, long long chunk)
 {
-        return site != FAULT_NONE && isal_hip_knob(ISAL_HIP_KNOB_FAULT) == site;
+        const long long fc = isal_hip_knob(ISAL_HIP_KNOB_FAULT_CHUNK);
+        return site != FAULT_NONE && isal_hip_knob(ISAL_HIP_KNOB_FAULT) == site &&
+               (fc < 0 || fc == chunk);
 }
 
-#define GPU_TRY_AT(r, site, call)                                                                  \
+#define GPU_TRY_ATC(r, site, chunk, call)                                                          \
         do {                                                                                       \
-                hipError_t e_ = fault_at(site) ? hipErrorOutOfMemory : (call);                     \
+                hipError_t e_ = fault_at(site, chunk) ? hipErrorOutOfMemory : (call);              \
                 if (e_ != hipSuccess) {                                                            \
                         (r).err = e_;                                                              \
                         (r).what = #call;                                                          \
                         return (r);                                                                \
                 }                                                                                  \
         } while (0)
+
+#define GPU_TRY_AT(r, site, call) GPU_TRY_ATC(r, site, 0, call)
 
 #define GPU_TRY(r, call)                                                                           \
         do {                                                                                       \
@@ -551,6 +634,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
         for (c0 = 0; c0 < len; c0 += (long long) chunk) {
                 int clen = (int) ((long long) len - c0 < (long long) chunk ? len - c0 : (long long) chunk);
                 int s = 0, vec16 = 1;
+                const long long ci = c0 / (long long) chunk;
                 for (i = 0; i < nptr; i++) {
                         unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
                         uint64_t d;
@@ -562,7 +646,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                                 /* sources, and outputs of a read-modify-write update or
                                  * of a verify, go in */
                                 if (i < nsrc || op != OP_ENCODE)
-                                        GPU_TRY_AT(r, FAULT_H2D, hipMemcpyAsync(st, host + c0, (size_t) clen,
+                                        GPU_TRY_ATC(r, FAULT_H2D, ci, hipMemcpyAsync(st, host + c0, (size_t) clen,
                                                                   hipMemcpyHostToDevice, c->stream));
                         }
                         h_ptrs[i] = d;
@@ -571,7 +655,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                 }
                 GPU_TRY(r, hipMemcpyAsync(c->d_args, c->h_args, L.args_bytes,
                                           hipMemcpyHostToDevice, c->stream));
-                GPU_TRY_AT(r, FAULT_LAUNCH, launch_op(c, op, (char *) c->d_args, &L, nptr, nsrc, clen, c0, k, rows,
+                GPU_TRY_ATC(r, FAULT_LAUNCH, ci, launch_op(c, op, (char *) c->d_args, &L, nptr, nsrc, clen, c0, k, rows,
                                      vec_i, vec16, &nslots));
                 if (op == OP_VERIFY) {
                         GPU_TRY(r, hipMemcpyAsync((char *) c->h_args + L.slots_off,
@@ -594,7 +678,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                         if (flag[i])
                                 continue;
                         if (i >= nsrc) {
-                                GPU_TRY_AT(r, i - nsrc == 1 ? FAULT_D2H : FAULT_NONE,
+                                GPU_TRY_ATC(r, i - nsrc == 1 ? FAULT_D2H : FAULT_NONE, ci,
                                            hipMemcpyAsync(dst[i - nsrc] + c0,
                                                           c->d_stage + (size_t) s * slot,
                                                           (size_t) clen, hipMemcpyDeviceToHost,
@@ -603,12 +687,316 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                         }
                         s++;
                 }
-                GPU_TRY_AT(r, FAULT_SYNC, hipStreamSynchronize(c->stream));
+                GPU_TRY_ATC(r, FAULT_SYNC, ci, hipStreamSynchronize(c->stream));
                 r.done = c0 + clen;
                 r.rows_out = 0;
         }
         r.done = len;
         return r;
+}
+
+/* Column-chunk bytes per shard of a pipelined call: ISAL_HIP_CHUNK_KB, else a
+ * quarter of the shard (so even a one-stripe call has chunks to overlap),
+ * between 512 KiB and DEFAULT_CHUNK_BYTES, in 4 KiB steps (a pageable copy
+ * has a fixed cost: 1 MiB copies run at 35 GB/s, 8 MiB ones at 52,
+ * profiles/r03_stage_probe.jsonl). */
+static size_t
+chunk_bytes(int len)
+{
+        const long long kb = isal_hip_knob(ISAL_HIP_KNOB_CHUNK_KB);
+        size_t c;
+        if (kb > 0)
+                return (size_t) kb << 10;
+        c = ((size_t) len / 4 + 4095) & ~(size_t) 4095;
+        if (c < ((size_t) 512 << 10))
+                c = (size_t) 512 << 10;
+        return c < DEFAULT_CHUNK_BYTES ? c : DEFAULT_CHUNK_BYTES;
+}
+
+/* Output copies of chunk ci (staging set ci % PIPE_NBUF) on s_out, after its
+ * kernel. *rows_out: output rows whose copy was enqueued. */
+static hipError_t
+copy_out_chunk(ctx_t *c, const outq_t *q, long long ci, const char **what, int *rows_out)
+{
+        const long long p0 = ci * (long long) q->chunk;
+        const int plen = (int) ((long long) q->len - p0 < (long long) q->chunk ? q->len - p0
+                                                                                : (long long) q->chunk);
+        const int b = (int) (ci % PIPE_NBUF);
+        unsigned char *stage = c->d_stage + (size_t) b * q->set_bytes;
+        hipError_t e;
+        int i, s = 0;
+        *rows_out = 0;
+        if ((e = hipStreamWaitEvent(c->s_out, c->ev_k[b], 0)) != hipSuccess) {
+                *what = "hipStreamWaitEvent(copy-out)";
+                return e;
+        }
+        for (i = 0; i < q->nptr; i++) {
+                if (q->flag[i])
+                        continue;
+                if (i >= q->nsrc) {
+                        e = fault_at(i - q->nsrc == 1 ? FAULT_D2H : FAULT_NONE, ci)
+                                    ? hipErrorOutOfMemory
+                                    : hipMemcpyAsync(q->dst[i - q->nsrc] + p0, stage + (size_t) s * q->slot,
+                                                     (size_t) plen, hipMemcpyDeviceToHost, c->s_out);
+                        if (e != hipSuccess) {
+                                *what = "hipMemcpyAsync(D2H chunk)";
+                                return e;
+                        }
+                        *rows_out = i - q->nsrc + 1;
+                }
+                s++;
+        }
+        if ((e = hipEventRecord(c->ev_out[b], c->s_out)) != hipSuccess)
+                *what = "hipEventRecord(copy-out)";
+        return e;
+}
+
+static void *
+outq_main(void *arg)
+{
+        ctx_t *c = (ctx_t *) arg;
+        outq_t *q = c->oq;
+        (void) hipSetDevice(c->device);
+        pthread_mutex_lock(&q->mu);
+        for (;;) {
+                long long ci;
+                const char *what = NULL;
+                int rows_out;
+                hipError_t e;
+                while (!q->quit && !(q->active && q->err == hipSuccess && q->handled < q->posted))
+                        pthread_cond_wait(&q->cv, &q->mu);
+                if (q->quit)
+                        break;
+                ci = q->handled;
+                pthread_mutex_unlock(&q->mu);
+                e = copy_out_chunk(c, q, ci, &what, &rows_out);
+                pthread_mutex_lock(&q->mu);
+                if (e != hipSuccess) {
+                        q->err = e;
+                        q->what = what;
+                        q->fail_chunk = ci;
+                        q->rows_out = rows_out;
+                } else {
+                        q->handled = ci + 1;
+                }
+                pthread_cond_broadcast(&q->cv);
+        }
+        pthread_mutex_unlock(&q->mu);
+        return NULL;
+}
+
+static hipError_t
+outq_start(ctx_t *c)
+{
+        outq_t *q;
+        if (c->oq)
+                return hipSuccess;
+        q = (outq_t *) calloc(1, sizeof(*q));
+        if (!q)
+                return hipErrorOutOfMemory;
+        pthread_mutex_init(&q->mu, NULL);
+        pthread_cond_init(&q->cv, NULL);
+        c->oq = q;
+        if (pthread_create(&q->th, NULL, outq_main, c) != 0) {
+                pthread_mutex_destroy(&q->mu);
+                pthread_cond_destroy(&q->cv);
+                free(q);
+                c->oq = NULL;
+                return hipErrorOutOfMemory;
+        }
+        return hipSuccess;
+}
+
+static void
+outq_stop(ctx_t *c)
+{
+        outq_t *q = c->oq;
+        pthread_mutex_lock(&q->mu);
+        q->quit = 1;
+        pthread_cond_broadcast(&q->cv);
+        pthread_mutex_unlock(&q->mu);
+        pthread_join(q->th, NULL);
+        pthread_mutex_destroy(&q->mu);
+        pthread_cond_destroy(&q->cv);
+        free(q);
+        c->oq = NULL;
+}
+
+/* Wait until the worker has enqueued the copies of chunks [0, n) or failed;
+ * returns its error. */
+static hipError_t
+outq_wait(outq_t *q, long long n)
+{
+        hipError_t e;
+        pthread_mutex_lock(&q->mu);
+        while (q->err == hipSuccess && q->handled < n)
+                pthread_cond_wait(&q->cv, &q->mu);
+        e = q->err;
+        pthread_mutex_unlock(&q->mu);
+        return e;
+}
+
+/*
+ * Pipelined column chunks: large host-resident encode / update calls. Chunk i
+ * flows through staging set i % PIPE_NBUF in HBM: H2D of its sources (and of
+ * its parity, for an update) on s_in, argument upload + kernel on the call's
+ * stream, D2H of its outputs on s_out, chained by events. The calling thread
+ * stages in and launches; the copy-out worker (outq) issues the D2H copies,
+ * so that the H2D of chunk i + 1, the kernel of chunk i and the D2H of chunk
+ * i - 1 run at once even for pageable host buffers. Host memory is written
+ * only by the D2H copies, in chunk order: r.done is the end of the last chunk
+ * whose output copies were all enqueued, rows_out counts the rows of the next
+ * chunk whose copy was enqueued when an enqueue failed (as gpu_chunked). The
+ * caller quiesces every stream before it trusts either.
+ */
+static gpu_res
+gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+              unsigned char *const *src, int nsrc, unsigned char *const *dst, const int *flag,
+              int nstage)
+{
+        gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
+        const int nptr = nsrc + rows;
+        size_t chunk = chunk_bytes(len), per, slot, set_bytes, astride;
+        long long nchunks, ci, launched = 0;
+        layout_t L;
+        outq_t *q;
+        int b, i;
+
+        per = stage_limit() / ((size_t) nstage * PIPE_NBUF) & ~(size_t) 4095;
+        if (chunk > per)
+                chunk = per < 4096 ? 4096 : per;
+        if (chunk > (size_t) len)
+                chunk = (size_t) len;
+        slot = (chunk + 255) & ~(size_t) 255;
+        set_bytes = slot * (size_t) nstage;
+        GPU_TRY_AT(r, FAULT_ALLOC, ensure_stage(c, set_bytes * PIPE_NBUF));
+        GPU_TRY_AT(r, FAULT_ALLOC, ensure_pipe(c));
+        GPU_TRY_AT(r, FAULT_ALLOC, outq_start(c));
+        L = call_layout(op, len, k, rows, nptr, 0);
+        astride = (L.args_bytes + 255) & ~(size_t) 255;
+        GPU_TRY_AT(r, FAULT_ALLOC, ensure_args(c, astride * PIPE_NBUF));
+        /* one argument region per staging set: pointer table + coefficient tables */
+        isal_hip_build_tables(k, rows, gftbls, (uint32_t *) ((char *) c->h_args + L.ptr_bytes));
+        for (b = 1; b < PIPE_NBUF; b++)
+                memcpy((char *) c->h_args + b * astride + L.ptr_bytes, (char *) c->h_args + L.ptr_bytes,
+                       L.args_bytes - L.ptr_bytes);
+        nchunks = ((long long) len + (long long) chunk - 1) / (long long) chunk;
+
+        q = c->oq;
+        pthread_mutex_lock(&q->mu);
+        q->op = op;
+        q->nsrc = nsrc;
+        q->nptr = nptr;
+        q->len = len;
+        q->flag = flag;
+        q->dst = dst;
+        q->chunk = chunk;
+        q->slot = slot;
+        q->set_bytes = set_bytes;
+        q->posted = q->handled = 0;
+        q->err = hipSuccess;
+        q->active = 1;
+        pthread_mutex_unlock(&q->mu);
+
+        for (ci = 0; ci < nchunks && r.err == hipSuccess; ci++) {
+                const long long c0 = ci * (long long) chunk;
+                const int clen = (int) ((long long) len - c0 < (long long) chunk ? len - c0 : (long long) chunk);
+                char *h, *dargs;
+                unsigned char *stage;
+                uint64_t *h_ptrs;
+                int s = 0, vec16 = 1, nslots;
+                hipError_t e = hipSuccess;
+                const char *what = NULL;
+                b = (int) (ci % PIPE_NBUF);
+                h = (char *) c->h_args + b * astride;
+                dargs = (char *) c->d_args + b * astride;
+                stage = c->d_stage + b * set_bytes;
+                h_ptrs = (uint64_t *) h;
+#define PIPE_STEP(site, call)                                                                      \
+        do {                                                                                       \
+                if (e == hipSuccess) {                                                             \
+                        e = fault_at(site, ci) ? hipErrorOutOfMemory : (call);                     \
+                        if (e != hipSuccess)                                                       \
+                                what = #call;                                                      \
+                }                                                                                  \
+        } while (0)
+                if (ci >= PIPE_NBUF) {
+                        /* staging set b is free once chunk ci - NBUF's parity has left it
+                         * (its copy-out event recorded), and argument region b once that
+                         * chunk's upload ran */
+                        if ((e = outq_wait(q, ci - PIPE_NBUF + 1)) != hipSuccess)
+                                break; /* the worker's failure, reported below */
+                        PIPE_STEP(FAULT_SYNC, hipEventSynchronize(c->ev_k[b]));
+                        PIPE_STEP(FAULT_NONE, hipStreamWaitEvent(c->s_in, c->ev_out[b], 0));
+                }
+                for (i = 0; i < nptr && e == hipSuccess; i++) {
+                        unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
+                        uint64_t d;
+                        if (flag[i]) {
+                                d = (uint64_t) (uintptr_t) (host + c0);
+                        } else {
+                                unsigned char *st = stage + (size_t) s++ * slot;
+                                d = (uint64_t) (uintptr_t) st;
+                                if (i < nsrc || op != OP_ENCODE)
+                                        PIPE_STEP(FAULT_H2D, hipMemcpyAsync(st, host + c0, (size_t) clen,
+                                                                            hipMemcpyHostToDevice, c->s_in));
+                        }
+                        h_ptrs[i] = d;
+                        if (d & 15)
+                                vec16 = 0;
+                }
+                PIPE_STEP(FAULT_NONE, hipEventRecord(c->ev_in[b], c->s_in));
+                PIPE_STEP(FAULT_NONE, hipStreamWaitEvent(c->stream, c->ev_in[b], 0));
+                PIPE_STEP(FAULT_NONE, hipMemcpyAsync(dargs, h, L.args_bytes, hipMemcpyHostToDevice, c->stream));
+                PIPE_STEP(FAULT_LAUNCH, (hipError_t) launch_op(c, op, dargs, &L, nptr, nsrc, clen, c0, k, rows,
+                                                               vec_i, vec16, &nslots));
+                PIPE_STEP(FAULT_NONE, hipEventRecord(c->ev_k[b], c->stream));
+#undef PIPE_STEP
+                if (e != hipSuccess) {
+                        r.err = e;
+                        r.what = what;
+                        break;
+                }
+                launched = ci + 1;
+                pthread_mutex_lock(&q->mu);
+                q->posted = launched;
+                pthread_cond_signal(&q->cv);
+                pthread_mutex_unlock(&q->mu);
+        }
+        /* let the worker finish the chunks that were launched (or fail) */
+        (void) outq_wait(q, launched);
+        pthread_mutex_lock(&q->mu);
+        q->active = 0;
+        if (q->err != hipSuccess) { /* the first failure in chunk order is the worker's */
+                r.err = q->err;
+                r.what = q->what;
+                r.done = q->fail_chunk * (long long) chunk;
+                r.chunk_end = r.done + (long long) chunk < len ? r.done + (long long) chunk : len;
+                r.rows_out = q->rows_out;
+        } else {
+                r.done = q->handled * (long long) chunk < len ? q->handled * (long long) chunk : len;
+                r.rows_out = 0;
+        }
+        pthread_mutex_unlock(&q->mu);
+        if (r.err != hipSuccess)
+                return r;
+        GPU_TRY_ATC(r, FAULT_SYNC, nchunks - 1, hipStreamSynchronize(c->s_out));
+        r.done = len;
+        return r;
+}
+
+/* Wait for everything a call queued; the first error, if any. */
+static hipError_t
+quiesce(ctx_t *c)
+{
+        hipError_t e = hipStreamSynchronize(c->stream), e2;
+        if (c->pipe_ready) {
+                if ((e2 = hipStreamSynchronize(c->s_in)) != hipSuccess && e == hipSuccess)
+                        e = e2;
+                if ((e2 = hipStreamSynchronize(c->s_out)) != hipSuccess && e == hipSuccess)
+                        e = e2;
+        }
+        return e;
 }
 
 static unsigned long long
@@ -686,9 +1074,12 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                           all_host ? "host shards" : "device shards");
                 r = gpu_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage, zc);
         } else {
-                route_log(op, len, k, rows, nstage ? "gpu chunked" : "gpu device-resident",
+                const int piped = nstage && op != OP_VERIFY && isal_hip_knob(ISAL_HIP_KNOB_PIPE_CHUNKS) != 0;
+                route_log(op, len, k, rows,
+                          piped ? "gpu pipelined chunks" : nstage ? "gpu chunked" : "gpu device-resident",
                           all_host ? "host shards" : "device shards");
-                r = gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage);
+                r = piped ? gpu_pipelined(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage)
+                          : gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage);
         }
         if (flag != dev_flag)
                 free(flag);
@@ -698,9 +1089,12 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 die(r.what, r.err);
         (void) hipGetLastError();
         report_fallback(r.what, r.err);
-        /* nothing queued may still write our outputs */
-        if (c && hipStreamSynchronize(c->stream) != hipSuccess && op == OP_UPDATE && r.rows_out)
-                die("hipStreamSynchronize after a failed update (parity state unknown)", r.err);
+        /* Nothing queued may still write our outputs: drain every stream of the
+         * call. Output copies into host memory were enqueued for [0, done) (and
+         * rows_out rows beyond); if the streams cannot be drained their state
+         * is unknown and no CPU result may be written over them. */
+        if (c && quiesce(c) != hipSuccess && (r.done > 0 || r.rows_out))
+                die("draining the streams after a failed call (output state unknown)", r.err);
         if (op == OP_UPDATE && r.rows_out) {
                 /* rows [0, rows_out) of [done, chunk_end) are already updated */
                 unsigned char *s1 = src[0] + r.done, **d1;

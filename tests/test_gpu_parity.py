@@ -386,6 +386,75 @@ def test_hip_failure_falls_back_to_cpu_route(engine, oracle, gpu, monkeypatch, s
             assert engine.fallbacks() > before, (site, n)
 
 
+@pytest.mark.parametrize("piped", ["1", "0"])
+@pytest.mark.parametrize("site", [2, 3, 4, 5])
+def test_hip_failure_in_a_later_chunk_resumes_on_cpu(engine, oracle, gpu, monkeypatch, site, piped):
+    """A HIP failure in column chunk 3 of a call (ISAL_HIP_FAULT_CHUNK): chunks
+    0-2 already went through the GPU, so the CPU route resumes at a column
+    > 0; an update that failed while copying chunk 3's parity back must not
+    fold the rows already copied a second time; RAID checks (the verify
+    kernel) must still find the first mismatch. Pipelined chunks
+    (ISAL_HIP_PIPE_CHUNKS=1, H2D / kernel / D2H of neighbouring chunks in
+    flight at once) and one-chunk-at-a-time (=0). Every result == oracle."""
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", "auto")
+    _setenv(monkeypatch, "ISAL_HIP_CPU_MAX_BYTES", "0")
+    _setenv(monkeypatch, "ISAL_HIP_STAGE_MB", "1")
+    _setenv(monkeypatch, "ISAL_HIP_CHUNK_KB", "64")
+    _setenv(monkeypatch, "ISAL_HIP_PIPE_CHUNKS", piped)
+    _setenv(monkeypatch, "ISAL_HIP_FAULT", str(site))
+    _setenv(monkeypatch, "ISAL_HIP_FAULT_CHUNK", "3")
+    rng = np.random.default_rng(site)
+    k, rows, n = 6, 5, 600000 + 16 * site  # 11 staged shards x n > 4 MiB: the chunked routes
+    coef = fill_bytes(k * rows, n)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    src = [fill_bytes(n, 31 * site + j) for j in range(k)]
+    want = oracle.encode(coef, k, rows, src)
+    before = engine.fallbacks()
+    got = [np.zeros(n, np.uint8) for _ in range(rows)]
+    engine.ec_encode_data(n, k, rows, tbls, src, got)
+    assert all(np.array_equal(a, b) for a, b in zip(got, want)), ("encode", site)
+    assert engine.fallbacks() > before, site
+    upd = [np.zeros(n, np.uint8) for _ in range(rows)]
+    for v in rng.permutation(k):
+        engine.ec_encode_data_update(n, k, rows, int(v), tbls, src[int(v)], upd)
+    assert all(np.array_equal(a, b) for a, b in zip(upd, want)), ("update", site)
+    # verify (xor_check / pq_check) with a corrupted byte in chunk 4
+    xc, pc = _raid_fn(engine, "xor_check"), _raid_fn(engine, "pq_check")
+    vec = [fill_bytes(n, 7 * site + j) for j in range(6)]
+    assert oracle.raid("pq_gen", 6, n, vec) == 0
+    pos = 4 * 28672 + 123 + site
+    vec[1][pos] ^= 0x5A
+    assert pc(6, n, _vp(vec)) == oracle.raid("pq_check", 6, n, [x.copy() for x in vec])
+    xv = [fill_bytes(n, 3 * site + j) for j in range(5)]
+    assert oracle.raid("xor_gen", 5, n, xv) == 0
+    xv[2][pos] ^= 1
+    assert xc(5, n, _vp(xv)) == oracle.raid("xor_check", 5, n, [x.copy() for x in xv])
+
+
+def test_large_host_call_pipelined_vs_oracle(engine, oracle, gpu, monkeypatch):
+    """A 64 MiB-per-shard synchronous call on pageable host buffers goes
+    through the pipelined column chunks (H2D / kernel / D2H of neighbouring
+    chunks overlapped); encode and a full update sequence == oracle."""
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", "auto")
+    _setenv(monkeypatch, "ISAL_HIP_LOG", "0")
+    k, rows, n = 4, 2, 64 << 20
+    coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+    tbls = engine.ec_init_tables(k, rows, coef)
+    src = [fill_bytes(n, 900 + j) for j in range(k)]
+    want = oracle.encode(coef, k, rows, src)
+    launches = engine.kernel_launches()
+    got = [np.zeros(n, np.uint8) for _ in range(rows)]
+    engine.ec_encode_data(n, k, rows, tbls, src, got)
+    assert engine.kernel_launches() >= launches + 64  # 1 MiB chunks: one launch each
+    for l in range(rows):
+        assert np.array_equal(got[l], want[l]), l
+    upd = [np.zeros(n, np.uint8) for _ in range(rows)]
+    for v in range(k):
+        engine.ec_encode_data_update(n, k, rows, v, tbls, src[v], upd)
+    for l in range(rows):
+        assert np.array_equal(upd[l], want[l]), ("update", l)
+
+
 def test_dropin_call_ordered_after_default_stream_work(engine, oracle, gpu):
     """A synchronous drop-in call on device shards sees work the caller queued
     on the legacy default stream just before it (torch writes the sources and
@@ -874,7 +943,7 @@ def test_encode_crc64_knobs(engine, oracle, gpu, monkeypatch, pair, chain, k, ro
 @pytest.mark.parametrize("slice_,pair,chain,nv", [
     ("1", 1, "lds", 1), ("1", 0, "lds", 1), ("1", 1, "reg", 1), ("1", 0, "reg", 1),
     ("1", 1, "lds", 2), ("1", 0, "lds", 2), ("0", 1, "lds", 2), ("0", 0, "lds", 2),
-    ("0", 1, "lds", 1), ("0", 1, "reg", 1)])
+    ("0", 1, "lds", 1), ("0", 1, "reg", 1), ("2", 1, "lds", 1), ("2", 1, "lds", 2), ("2", 0, "lds", 2)])
 @pytest.mark.parametrize("k,rows,n,ns,skew,tt,variant", ENCODE_CRC64_SHAPES[:5])
 def test_encode_crc64_slice_knobs(engine, oracle, gpu, monkeypatch, slice_, pair, chain, nv, k, rows, n,
                                   ns, skew, tt, variant):
@@ -889,11 +958,12 @@ def test_encode_crc64_slice_knobs(engine, oracle, gpu, monkeypatch, slice_, pair
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant)
 
 
-@pytest.mark.parametrize("slice_", ["0", "1"])
+@pytest.mark.parametrize("slice_", ["0", "1", "2"])
 @pytest.mark.parametrize("variant", range(8))
 def test_encode_crc64_every_flavour(engine, oracle, gpu, monkeypatch, variant, slice_):
-    """All eight crc64.h flavours through the fused kernel, field-table and
-    slicing paths (the slicing path byte-swaps the norm flavours' chains)."""
+    """All eight crc64.h flavours through the fused kernel, field-table,
+    slicing and hybrid paths (the u-domain paths byte-swap the norm flavours'
+    chains; the hybrid tables exist for load group 10, i.e. the k = 10 case)."""
     _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", slice_)
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 10, 4, 4096 * 37 + 2048, 3, 0, 4,
                                 variant)

@@ -40,6 +40,22 @@ for s in $STEPS; do
                 # how a synchronous host-resident call can move pageable shards (tools/stage_probe.c)
                 run stage_probe 300 tools/stage_probe
                 ;;
+        faulttests)
+                run pytest_gpu_fault 600 python -u -m pytest tests -m gpu -x -v -k "hip_failure or large_host_call or multi_device" --timeout 300 --timeout-method thread
+                ;;
+        hybrid)
+                # fused encode+CRC64: byte tables (1) vs hybrid byte/field tables (2), LDS counters of each
+                run pytest_gpu_hybrid 900 python -u -m pytest tests -m gpu -x -v -k "encode_crc64_slice_knobs or encode_crc64_every_flavour" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for sl in 1 2; do
+                                ISAL_HIP_CRC64_SLICE=$sl run bench_encrc64_sl${sl}_r$r 300 python bench.py --workload encode-crc64 --no-cpu-baseline
+                        done
+                done
+                for sl in 1 2; do
+                        ISAL_HIP_CRC64_SLICE=$sl run pmc_lds_encrc64_sl$sl 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_encrc64_sl$sl" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
+                        ISAL_HIP_CRC64_SLICE=$sl run rocprof_encrc64_sl$sl 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_encrc64_sl$sl" -o e -- python3 bench.py --workload encode-crc64 --no-cpu-baseline
+                done
+                ;;
         fuzzgpu)
                 # differential fuzzing of the shipped library on the kernels (tests/fuzz)
                 python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
@@ -245,6 +261,9 @@ for s in $STEPS; do
         c5)
                 run bench_c5 600 python bench.py --total-stripes 1048576 --steps 2 --warmup 1
                 cp "$OUT/bench_c5.log" "$OUT/bench_c5.json"
+                ;;
+        chunks)
+                run chunk_sweep 300 python tools/chunk_sweep.py
                 ;;
         route)
                 run route_crossover 300 python tools/route_crossover.py

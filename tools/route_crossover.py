@@ -3,11 +3,13 @@
 
 Times one synchronous ec_encode_data call on HOST-resident shards (k=10, p=4,
 plain pageable numpy buffers — what a storage daemon hands the reference) at
-shard lengths from 1 KiB to 4 MiB, forced onto the CPU route
-(ISAL_HIP_BACKEND=cpu) and onto the GPU (=gpu), and prints the per-call times
+shard lengths from 1 KiB to 16 MiB, forced onto the CPU route
+(ISAL_HIP_BACKEND=cpu, up to 4 MiB) and onto the GPU (=gpu), and prints the per-call times
 and the byte count (k + p) * len where the GPU starts to win. That count is
 DEFAULT_CPU_MAX_BYTES in isal_hip_shim.c. Also times hipPointerGetAttributes,
-the per-pointer classification cost every routed call pays.
+the per-pointer classification cost every routed call pays. From 1 MiB shards on
+it also times the chunked GPU route one chunk at a time
+(ISAL_HIP_PIPE_CHUNKS=0, the round-2 behaviour) and with page-locked buffers.
 """
 import ctypes
 import json
@@ -22,12 +24,17 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import isal_amd  # noqa: E402
 
 
-def per_call(k, p, n, backend, budget=0.5):
+def per_call(k, p, n, backend, budget=0.5, piped="1", pinned=False):
     os.environ["ISAL_HIP_BACKEND"] = backend
+    os.environ["ISAL_HIP_PIPE_CHUNKS"] = piped
     isal_amd.reload_config()
     rng = np.random.default_rng(n)
-    src = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
-    dst = [np.zeros(n, np.uint8) for _ in range(p)]
+    if pinned:  # page-locked host buffers (torch pin_memory = hipHostMalloc)
+        src = [torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8)).pin_memory().numpy() for _ in range(k)]
+        dst = [torch.zeros(n, dtype=torch.uint8).pin_memory().numpy() for _ in range(p)]
+    else:
+        src = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+        dst = [np.zeros(n, np.uint8) for _ in range(p)]
     a = isal_amd.gf_gen_rs_matrix(k + p, k)
     tbls = isal_amd.ec_init_tables(k, p, a[k * k:])
     L = isal_amd.lib()
@@ -45,11 +52,18 @@ def main():
     k, p = 10, 4
     rows = []
     crossover = None
-    for n in [1 << e for e in range(10, 23)]:
-        cpu, gpu = per_call(k, p, n, "cpu"), per_call(k, p, n, "gpu")
-        rows.append({"len": n, "bytes": (k + p) * n, "cpu_us": round(cpu, 1), "gpu_us": round(gpu, 1)})
+    for n in [1 << e for e in range(10, 25)]:
+        cpu = per_call(k, p, n, "cpu") if n <= 1 << 22 else None
+        gpu = per_call(k, p, n, "gpu")
+        row = {"len": n, "bytes": (k + p) * n, "cpu_us": cpu and round(cpu, 1), "gpu_us": round(gpu, 1)}
+        if n >= 1 << 20:  # the chunked route: pipelined (default) vs one chunk at a time, pinned buffers
+            row["gpu_unpipelined_us"] = round(per_call(k, p, n, "gpu", piped="0"), 1)
+            row["gpu_pinned_us"] = round(per_call(k, p, n, "gpu", pinned=True), 1)
+            row["gpu_gb_s"] = round((k + p) * n / gpu / 1e3, 2)
+            row["gpu_pinned_gb_s"] = round((k + p) * n / row["gpu_pinned_us"] / 1e3, 2)
+        rows.append(row)
         print(json.dumps(rows[-1]), flush=True)
-        if crossover is None and gpu < cpu:
+        if crossover is None and cpu is not None and gpu < cpu:
             crossover = (k + p) * n
     hip = ctypes.CDLL("libamdhip64.so")
     attr = ctypes.create_string_buffer(64)
