@@ -262,6 +262,9 @@ for s in $STEPS; do
                 run bench_c5 600 python bench.py --total-stripes 1048576 --steps 2 --warmup 1
                 cp "$OUT/bench_c5.log" "$OUT/bench_c5.json"
                 ;;
+        calltrace)
+                run calltrace 300 rocprofv3 --memory-copy-trace --kernel-trace --output-format csv -d "$OUT/calltrace" -o t -- python3 tools/host_call_trace.py
+                ;;
         chunks)
                 run chunk_sweep 300 python tools/chunk_sweep.py
                 ;;
