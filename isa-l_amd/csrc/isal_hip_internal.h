@@ -113,6 +113,7 @@ enum {
         ISAL_HIP_KNOB_FAULT_CHUNK,     /* ... only in this column chunk of a call (tests; unset: every chunk) */
         ISAL_HIP_KNOB_CHUNK_KB,        /* column-chunk bytes per shard of large host calls (pipelined) */
         ISAL_HIP_KNOB_PIPE_CHUNKS,     /* 0: large host calls one chunk at a time (no copy overlap) */
+        ISAL_HIP_KNOB_PINNED_DIRECT,   /* 0: stage page-locked host shards like pageable ones */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

@@ -48,6 +48,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_FAULT_CHUNK] = {"ISAL_HIP_FAULT_CHUNK", NULL},
         [ISAL_HIP_KNOB_CHUNK_KB] = {"ISAL_HIP_CHUNK_KB", NULL},
         [ISAL_HIP_KNOB_PIPE_CHUNKS] = {"ISAL_HIP_PIPE_CHUNKS", NULL},
+        [ISAL_HIP_KNOB_PINNED_DIRECT] = {"ISAL_HIP_PINNED_DIRECT", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];

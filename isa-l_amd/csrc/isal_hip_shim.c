@@ -171,7 +171,7 @@ gpu_present(void)
  * (override: ISAL_HIP_CHUNK_KB) that flow through PIPE_NBUF staging buffers:
  * the H2D copy of chunk i+1, the kernel of chunk i and the D2H copy of chunk
  * i-1 run at once on three streams. */
-#define DEFAULT_CHUNK_BYTES ((size_t) 1 << 20)
+#define DEFAULT_CHUNK_BYTES ((size_t) 4 << 20)
 #define PIPE_NBUF 3
 
 typedef struct {
@@ -204,7 +204,7 @@ typedef struct outq {
         long long posted, handled; /* chunks launched / whose output copies are enqueued */
         /* the call being served */
         int op, nsrc, nptr, len;
-        const int *flag;
+        const uint64_t *view;
         unsigned char *const *dst;
         size_t chunk, slot, set_bytes;
         /* the worker's first failure */
@@ -381,11 +381,19 @@ stage_limit(void)
 
 /* ---- pointer classification ------------------------------------------- */
 
-static int
-on_device(const void *p)
+/* Where a shard lives, as the kernels see it. Device (hipMalloc) and managed
+ * memory: the pointer itself. Page-locked host memory (hipHostMalloc,
+ * hipHostRegister — NIC / disk DMA buffers usually are): the device's mapping
+ * of it, so kernels read and write it in place over PCIe with no staging copy
+ * (ISAL_HIP_PINNED_DIRECT=0 stages it like pageable memory). Pageable
+ * memory: 0 — it must be copied through a staging buffer. *is_dev tells
+ * device memory (which no CPU route can read) from host memory. */
+static uint64_t
+classify(const void *p, int *is_dev)
 {
         hipPointerAttribute_t a;
         hipError_t e;
+        *is_dev = 0;
         if (!p)
                 return 0;
         e = hipPointerGetAttributes(&a, p);
@@ -393,8 +401,18 @@ on_device(const void *p)
                 (void) hipGetLastError(); /* unknown to HIP: plain host memory */
                 return 0;
         }
-        return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
-               a.type == hipMemoryTypeUnified;
+        if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+            a.type == hipMemoryTypeUnified) {
+                *is_dev = 1;
+                return (uint64_t) (uintptr_t) p;
+        }
+        if (a.type == hipMemoryTypeHost && a.devicePointer &&
+            isal_hip_knob(ISAL_HIP_KNOB_PINNED_DIRECT) != 0) {
+                /* attributes describe p itself (the mapping of the allocation
+                 * base plus p's offset into it) */
+                return (uint64_t) (uintptr_t) a.devicePointer;
+        }
+        return 0;
 }
 
 /* ---- the generic synchronous call --------------------------------------- */
@@ -535,7 +553,7 @@ fault_at(int site, long long chunk)
  * written only after the stream completed, so a failure leaves them untouched. */
 static gpu_res
 gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
-          unsigned char *const *src, int nsrc, unsigned char *const *dst, const int *flag,
+          unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
           int nstage, int zero_copy)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
@@ -554,8 +572,8 @@ gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
         for (i = 0, s = 0; i < nptr; i++) {
                 unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
                 uint64_t d;
-                if (flag[i]) {
-                        d = (uint64_t) (uintptr_t) host;
+                if (view[i]) {
+                        d = view[i];
                 } else {
                         d = (uint64_t) (uintptr_t) (dv + L.stage_off + (size_t) s * L.slot);
                         if (i < nsrc || op != OP_ENCODE) {
@@ -590,7 +608,7 @@ gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
                 r.first_bad = min_slot((const unsigned long long *) (h + L.slots_off), nslots);
         } else {
                 for (i = nsrc, s = first_out; i < nptr && s >= 0; i++)
-                        if (!flag[i])
+                        if (!view[i])
                                 memcpy(dst[i - nsrc], h + L.stage_off + (size_t) s++ * L.slot,
                                        (size_t) len);
         }
@@ -603,7 +621,7 @@ gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
  * chunk whose outputs are final. */
 static gpu_res
 gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
-            unsigned char *const *src, int nsrc, unsigned char *const *dst, const int *flag,
+            unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
             int nstage)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
@@ -638,8 +656,8 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                 for (i = 0; i < nptr; i++) {
                         unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
                         uint64_t d;
-                        if (flag[i]) {
-                                d = (uint64_t) (uintptr_t) (host + c0);
+                        if (view[i]) {
+                                d = view[i] + (uint64_t) c0;
                         } else {
                                 unsigned char *st = c->d_stage + (size_t) s++ * slot;
                                 d = (uint64_t) (uintptr_t) st;
@@ -675,7 +693,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                 r.chunk_end = c0 + clen;
                 r.rows_out = 0;
                 for (i = 0; i < nptr; i++) {
-                        if (flag[i])
+                        if (view[i])
                                 continue;
                         if (i >= nsrc) {
                                 GPU_TRY_ATC(r, i - nsrc == 1 ? FAULT_D2H : FAULT_NONE, ci,
@@ -695,22 +713,17 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
         return r;
 }
 
-/* Column-chunk bytes per shard of a pipelined call: ISAL_HIP_CHUNK_KB, else a
- * quarter of the shard (so even a one-stripe call has chunks to overlap),
- * between 512 KiB and DEFAULT_CHUNK_BYTES, in 4 KiB steps (a pageable copy
- * has a fixed cost: 1 MiB copies run at 35 GB/s, 8 MiB ones at 52,
- * profiles/r03_stage_probe.jsonl). */
+/* Column-chunk bytes per shard of a pipelined call: ISAL_HIP_CHUNK_KB, else
+ * DEFAULT_CHUNK_BYTES. Every chunk costs one copy per staged shard each way,
+ * and a copy from or to pageable memory has a fixed cost of ~14 us beside its
+ * bytes (profiles/r03_calltrace.txt), so chunks must be large: at 16 MiB
+ * shards 4 MiB chunks beat one chunk by 4-9 %, 1 MiB chunks lose 50 %
+ * (profiles/r03_chunk_sweep*.jsonl). */
 static size_t
-chunk_bytes(int len)
+chunk_bytes(void)
 {
         const long long kb = isal_hip_knob(ISAL_HIP_KNOB_CHUNK_KB);
-        size_t c;
-        if (kb > 0)
-                return (size_t) kb << 10;
-        c = ((size_t) len / 4 + 4095) & ~(size_t) 4095;
-        if (c < ((size_t) 512 << 10))
-                c = (size_t) 512 << 10;
-        return c < DEFAULT_CHUNK_BYTES ? c : DEFAULT_CHUNK_BYTES;
+        return kb > 0 ? (size_t) kb << 10 : DEFAULT_CHUNK_BYTES;
 }
 
 /* Output copies of chunk ci (staging set ci % PIPE_NBUF) on s_out, after its
@@ -731,7 +744,7 @@ copy_out_chunk(ctx_t *c, const outq_t *q, long long ci, const char **what, int *
                 return e;
         }
         for (i = 0; i < q->nptr; i++) {
-                if (q->flag[i])
+                if (q->view[i])
                         continue;
                 if (i >= q->nsrc) {
                         e = fault_at(i - q->nsrc == 1 ? FAULT_D2H : FAULT_NONE, ci)
@@ -851,12 +864,12 @@ outq_wait(outq_t *q, long long n)
  */
 static gpu_res
 gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
-              unsigned char *const *src, int nsrc, unsigned char *const *dst, const int *flag,
+              unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
               int nstage)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         const int nptr = nsrc + rows;
-        size_t chunk = chunk_bytes(len), per, slot, set_bytes, astride;
+        size_t chunk = chunk_bytes(), per, slot, set_bytes, astride;
         long long nchunks, ci, launched = 0;
         layout_t L;
         outq_t *q;
@@ -865,8 +878,8 @@ gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsig
         per = stage_limit() / ((size_t) nstage * PIPE_NBUF) & ~(size_t) 4095;
         if (chunk > per)
                 chunk = per < 4096 ? 4096 : per;
-        if (chunk > (size_t) len)
-                chunk = (size_t) len;
+        if (chunk >= (size_t) len) /* one chunk: nothing to overlap */
+                return gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage);
         slot = (chunk + 255) & ~(size_t) 255;
         set_bytes = slot * (size_t) nstage;
         GPU_TRY_AT(r, FAULT_ALLOC, ensure_stage(c, set_bytes * PIPE_NBUF));
@@ -888,7 +901,7 @@ gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsig
         q->nsrc = nsrc;
         q->nptr = nptr;
         q->len = len;
-        q->flag = flag;
+        q->view = view;
         q->dst = dst;
         q->chunk = chunk;
         q->slot = slot;
@@ -932,8 +945,8 @@ gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsig
                 for (i = 0; i < nptr && e == hipSuccess; i++) {
                         unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
                         uint64_t d;
-                        if (flag[i]) {
-                                d = (uint64_t) (uintptr_t) (host + c0);
+                        if (view[i]) {
+                                d = view[i] + (uint64_t) c0;
                         } else {
                                 unsigned char *st = stage + (size_t) s++ * slot;
                                 d = (uint64_t) (uintptr_t) st;
@@ -1020,7 +1033,8 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
 {
         const int be = backend();
         const int nptr = nsrc + rows;
-        int dev_flag[512], *flag, i, nstage = 0, all_host;
+        uint64_t view_buf[512], *view;
+        int i, nstage = 0, ndev = 0, all_host;
         size_t bytes;
         gpu_res r;
         ctx_t *c;
@@ -1045,21 +1059,29 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 return cpu_route(op, 0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
         }
 
-        flag = nptr <= 512 ? dev_flag : (int *) malloc(sizeof(int) * (size_t) nptr);
-        if (!flag) {
+        view = nptr <= 512 ? view_buf : (uint64_t *) malloc(sizeof(uint64_t) * (size_t) nptr);
+        if (!view) {
                 fprintf(stderr, "isal_hip: out of host memory\n");
                 abort();
         }
         for (i = 0; i < nptr; i++) {
                 const void *p = i < nsrc ? src[i] : dst[i - nsrc];
-                flag[i] = on_device(p);
-                nstage += !flag[i];
+                int is_dev;
+                view[i] = classify(p, &is_dev);
+                /* An update's parity in page-locked host memory is staged, not
+                 * written in place: a kernel that failed after it started could
+                 * have folded some of it already, and the CPU fallback could not
+                 * tell which bytes. (Encode overwrites, verify only reads.) */
+                if (op == OP_UPDATE && i >= nsrc && view[i] && !is_dev)
+                        view[i] = 0;
+                ndev += is_dev;
+                nstage += !view[i];
         }
-        all_host = nstage == nptr;
+        all_host = ndev == 0;
 
         if (all_host && (be == BACKEND_CPU || (be == BACKEND_AUTO && bytes <= cpu_max_bytes()))) {
-                if (flag != dev_flag)
-                        free(flag);
+                if (view != view_buf)
+                        free(view);
                 route_log(op, len, k, rows, "cpu", be == BACKEND_CPU ? "ISAL_HIP_BACKEND=cpu" : "small host call");
                 return cpu_route(op, 0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
         }
@@ -1072,17 +1094,17 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 const int zc = bytes <= ZC_BYTES;
                 route_log(op, len, k, rows, zc ? "gpu zero-copy" : "gpu packed",
                           all_host ? "host shards" : "device shards");
-                r = gpu_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage, zc);
+                r = gpu_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, zc);
         } else {
                 const int piped = nstage && op != OP_VERIFY && isal_hip_knob(ISAL_HIP_KNOB_PIPE_CHUNKS) != 0;
                 route_log(op, len, k, rows,
-                          piped ? "gpu pipelined chunks" : nstage ? "gpu chunked" : "gpu device-resident",
+                          piped ? "gpu pipelined chunks" : nstage ? "gpu chunked" : "gpu direct (no staging)",
                           all_host ? "host shards" : "device shards");
-                r = piped ? gpu_pipelined(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage)
-                          : gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, flag, nstage);
+                r = piped ? gpu_pipelined(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage)
+                          : gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage);
         }
-        if (flag != dev_flag)
-                free(flag);
+        if (view != view_buf)
+                free(view);
         if (r.err == hipSuccess)
                 return r.first_bad;
         if (!all_host || be == BACKEND_GPU)

@@ -41,7 +41,7 @@ for s in $STEPS; do
                 run stage_probe 300 tools/stage_probe
                 ;;
         faulttests)
-                run pytest_gpu_fault 600 python -u -m pytest tests -m gpu -x -v -k "hip_failure or large_host_call or multi_device" --timeout 300 --timeout-method thread
+                run pytest_gpu_fault 600 python -u -m pytest tests -m gpu -x -v -k "hip_failure or large_host_call or multi_device or pinned_host" --timeout 300 --timeout-method thread
                 ;;
         hybrid)
                 # fused encode+CRC64: byte tables (1) vs hybrid byte/field tables (2), LDS counters of each
@@ -261,6 +261,9 @@ for s in $STEPS; do
         c5)
                 run bench_c5 600 python bench.py --total-stripes 1048576 --steps 2 --warmup 1
                 cp "$OUT/bench_c5.log" "$OUT/bench_c5.json"
+                ;;
+        zc)
+                run zc_probe 300 python tools/zc_probe.py
                 ;;
         calltrace)
                 run calltrace 300 rocprofv3 --memory-copy-trace --kernel-trace --output-format csv -d "$OUT/calltrace" -o t -- python3 tools/host_call_trace.py
