@@ -1401,7 +1401,7 @@ def test_differential_fuzz_on_the_kernels(gpu, tmp_path):
     subprocess.run([sys.executable, os.path.join(ecutil.REPO, "tests", "fuzz", "seeds.py"), "diff", str(corpus)],
                    check=True, capture_output=True)
     env = dict(os.environ, ISAL_HIP_BACKEND="gpu")
-    r = subprocess.run([exe, "-max_total_time=45", "-max_len=300000", "-print_final_stats=1",
+    r = subprocess.run([exe, "-max_total_time=45", "-max_len=300000", "-print_final_stats=1", "-rss_limit_mb=0",
                         f"-artifact_prefix={tmp_path}/", str(corpus)],
                        capture_output=True, text=True, timeout=240, env=env, cwd=tmp_path)
     out = r.stdout + r.stderr

@@ -40,6 +40,9 @@ for s in $STEPS; do
                 # how a synchronous host-resident call can move pageable shards (tools/stage_probe.c)
                 run stage_probe 300 tools/stage_probe
                 ;;
+        tail)
+                run pytest_gpu_tail 900 python -u -m pytest tests -m gpu -x -v -k "fuzz or bench or multi_device or pinned_host or hip_failure or large_host" --timeout 300 --timeout-method thread
+                ;;
         faulttests)
                 run pytest_gpu_fault 600 python -u -m pytest tests -m gpu -x -v -k "hip_failure or large_host_call or multi_device or pinned_host" --timeout 300 --timeout-method thread
                 ;;
@@ -59,7 +62,7 @@ for s in $STEPS; do
         fuzzgpu)
                 # differential fuzzing of the shipped library on the kernels (tests/fuzz)
                 python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
-                ISAL_HIP_BACKEND=gpu run fuzz_gpu 200 isa-l_amd/build/fuzzgpu/ec_diff_fuzz_gpu -max_total_time=90 -max_len=300000 -print_final_stats=1 -print_pcs=0 "$OUT/fuzz_corpus"
+                ISAL_HIP_BACKEND=gpu run fuzz_gpu 200 isa-l_amd/build/fuzzgpu/ec_diff_fuzz_gpu -max_total_time=90 -max_len=300000 -print_final_stats=1 -print_pcs=0 -rss_limit_mb=0 "$OUT/fuzz_corpus"
                 rm -rf "$OUT/fuzz_corpus"
                 ;;
         gpus2)

@@ -51,16 +51,19 @@ def per_call(k, p, n, backend, budget=0.5, piped="1", pinned=False):
 def main():
     k, p = 10, 4
     rows = []
-    crossover = None
+    crossover = pinned_crossover = None
     for n in [1 << e for e in range(10, 25)]:
         cpu = per_call(k, p, n, "cpu") if n <= 1 << 22 else None
         gpu = per_call(k, p, n, "gpu")
         row = {"len": n, "bytes": (k + p) * n, "cpu_us": cpu and round(cpu, 1), "gpu_us": round(gpu, 1)}
-        if n >= 1 << 20:  # the chunked route: pipelined (default) vs one chunk at a time, pinned buffers
+        # page-locked buffers: the kernels use them in place (no staging copy)
+        row["gpu_pinned_us"] = round(per_call(k, p, n, "gpu", pinned=True), 1)
+        row["gpu_pinned_gb_s"] = round((k + p) * n / row["gpu_pinned_us"] / 1e3, 2)
+        if n >= 1 << 20:  # the chunked route: pipelined (default) vs one chunk at a time
             row["gpu_unpipelined_us"] = round(per_call(k, p, n, "gpu", piped="0"), 1)
-            row["gpu_pinned_us"] = round(per_call(k, p, n, "gpu", pinned=True), 1)
             row["gpu_gb_s"] = round((k + p) * n / gpu / 1e3, 2)
-            row["gpu_pinned_gb_s"] = round((k + p) * n / row["gpu_pinned_us"] / 1e3, 2)
+        if pinned_crossover is None and cpu is not None and row["gpu_pinned_us"] < cpu:
+            pinned_crossover = (k + p) * n
         rows.append(row)
         print(json.dumps(rows[-1]), flush=True)
         if crossover is None and cpu is not None and gpu < cpu:
@@ -73,6 +76,7 @@ def main():
         hip.hipPointerGetAttributes(attr, ctypes.c_void_p(buf.ctypes.data))
     cls = (time.perf_counter() - t0) / 20000 * 1e6
     print(json.dumps({"first_len_where_gpu_wins_bytes": crossover,
+                      "first_len_where_gpu_wins_pinned_bytes": pinned_crossover,
                       "hipPointerGetAttributes_host_us": round(cls, 2)}), flush=True)
 
 

@@ -102,6 +102,32 @@ t_2thr(void)
         return now() - t0;
 }
 
+/* H2D of the k sources split over two host threads / two streams (even
+ * shards on s1 from this thread, odd shards on s2 from a helper): does a
+ * second issuing thread hide the per-copy cost? */
+static void *
+h2d_odd_thread(void *arg)
+{
+        (void) arg;
+        for (int j = 1; j < K; j += 2)
+                CK(hipMemcpyAsync(ds[j], hs[j], len, hipMemcpyHostToDevice, s2));
+        CK(hipStreamSynchronize(s2));
+        return NULL;
+}
+
+static double
+t_h2d_2thr(void)
+{
+        pthread_t th;
+        double t0 = now();
+        pthread_create(&th, NULL, h2d_odd_thread, NULL);
+        for (int j = 0; j < K; j += 2)
+                CK(hipMemcpyAsync(ds[j], hs[j], len, hipMemcpyHostToDevice, s1));
+        CK(hipStreamSynchronize(s1));
+        pthread_join(th, NULL);
+        return now() - t0;
+}
+
 static double
 t_reg(void)
 {
@@ -189,6 +215,7 @@ main(int argc, char **argv)
                 for (int i = 0; i < K; i++)
                         memcpy(pin + (i & 3) * (8 << 20), hs[i], len);
                 double m1 = now();
+                double h2d2 = best(t_h2d_2thr, 5);
                 double seq = best(t_seq, 5), h2d = best(t_h2d_only, 5), thr = best(t_2thr, 5),
                        reg = best(t_reg, 3);
                 double bnc[3];
@@ -207,11 +234,11 @@ main(int argc, char **argv)
                        "\"two_threads_us\": %.1f, \"two_threads_gb_s\": %.1f, "
                        "\"register_all_2streams_us\": %.1f, "
                        "\"bounce_h2d_gb_s_256k\": %.1f, \"bounce_h2d_gb_s_1m\": %.1f, "
-                       "\"bounce_h2d_gb_s_2m\": %.1f}\n",
+                       "\"bounce_h2d_gb_s_2m\": %.1f, \"h2d_two_threads_gb_s\": %.1f}\n",
                        len, mb, (a1 - a0) * 1e6, (a2 - a0) * 1e6, (a3 - a2) * 1e6, (a4 - a2) * 1e6,
                        (r1 - r0) * 1e6, (r2 - r1) * 1e6, mbin / (m1 - m0) / 1e3, seq * 1e6,
                        mb / seq / 1e3, mbin / h2d / 1e3, thr * 1e6, mb / thr / 1e3, reg * 1e6,
-                       mbin / bnc[0] / 1e3, mbin / bnc[1] / 1e3, mbin / bnc[2] / 1e3);
+                       mbin / bnc[0] / 1e3, mbin / bnc[1] / 1e3, mbin / bnc[2] / 1e3, mbin / h2d2 / 1e3);
                 fflush(stdout);
                 for (int i = 0; i < K + P; i++) {
                         free(hs[i]);
