@@ -141,6 +141,23 @@ cpu_max_bytes(void)
         return v >= 0 ? (size_t) v : DEFAULT_CPU_MAX_BYTES;
 }
 
+/* The same limit for calls whose host shards are all page-locked and used in
+ * place by the kernels (no staging copy): there the GPU wins from 1.8 MB
+ * (k = 10, p = 4: 51.6 vs 59.1 us; 14.7 MB: 290 vs 497 us,
+ * profiles/r03_route_crossover_c.jsonl). Override: ISAL_HIP_CPU_MAX_BYTES_PINNED
+ * (ISAL_HIP_CPU_MAX_BYTES also lowers it). */
+#define DEFAULT_CPU_MAX_BYTES_PINNED ((size_t) 2 << 20)
+
+static size_t
+cpu_max_bytes_pinned(void)
+{
+        const long long v = isal_hip_knob(ISAL_HIP_KNOB_CPU_MAX_BYTES_PINNED);
+        const size_t all = cpu_max_bytes();
+        if (v >= 0)
+                return (size_t) v;
+        return all < DEFAULT_CPU_MAX_BYTES_PINNED ? all : DEFAULT_CPU_MAX_BYTES_PINNED;
+}
+
 /* Is a GPU usable at all? (Asked once: a host without one, or without a
  * working driver, serves every host-resident call on the CPU route.) */
 static int gpu_ok;
@@ -1079,7 +1096,9 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         }
         all_host = ndev == 0;
 
-        if (all_host && (be == BACKEND_CPU || (be == BACKEND_AUTO && bytes <= cpu_max_bytes()))) {
+        if (all_host && (be == BACKEND_CPU ||
+                         (be == BACKEND_AUTO &&
+                          bytes <= (nstage == 0 ? cpu_max_bytes_pinned() : cpu_max_bytes())))) {
                 if (view != view_buf)
                         free(view);
                 route_log(op, len, k, rows, "cpu", be == BACKEND_CPU ? "ISAL_HIP_BACKEND=cpu" : "small host call");

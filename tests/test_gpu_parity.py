@@ -482,6 +482,34 @@ def test_pinned_host_shards_read_in_place(engine, oracle, gpu, monkeypatch, capf
     assert pc(6, n - 40, _vp(vec)) == oracle.raid("pq_check", 6, n - 40, [x.copy() for x in vec])
 
 
+def test_pinned_calls_take_the_gpu_earlier(engine, oracle, gpu, monkeypatch, capfd):
+    """Routing under ISAL_HIP_BACKEND=auto: a 3.7 MB k=10 p=4 call stays on the
+    CPU route from pageable buffers (the staged GPU route loses below ~29 MB)
+    but goes to the GPU when every shard is page-locked (used in place, the
+    GPU wins from ~1.8 MB); both == oracle."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", "auto")
+    _setenv(monkeypatch, "ISAL_HIP_LOG", "1")
+    k, p, n = 10, 4, 262144
+    coef = engine.gf_gen_rs_matrix(k + p, k)[k * k:]
+    tbls = engine.ec_init_tables(k, p, coef)
+    src = [fill_bytes(n, 40 + j) for j in range(k)]
+    want = oracle.encode(coef, k, p, src)
+    for pinned in (False, True):
+        if pinned:
+            s = [torch.from_numpy(x).pin_memory().numpy() for x in src]
+            out = [torch.zeros(n, dtype=torch.uint8).pin_memory().numpy() for _ in range(p)]
+        else:
+            s, out = src, [np.zeros(n, np.uint8) for _ in range(p)]
+        capfd.readouterr()
+        engine.ec_encode_data(n, k, p, tbls, s, out)
+        err = capfd.readouterr().err
+        assert ("-> gpu" in err) == pinned and ("-> cpu" in err) == (not pinned), err
+        for l in range(p):
+            assert np.array_equal(out[l], want[l]), (pinned, l)
+
+
 def test_large_host_call_pipelined_vs_oracle(engine, oracle, gpu, monkeypatch):
     """A 64 MiB-per-shard synchronous call on pageable host buffers goes
     through the pipelined column chunks (H2D / kernel / D2H of neighbouring

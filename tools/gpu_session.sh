@@ -41,7 +41,7 @@ for s in $STEPS; do
                 run stage_probe 300 tools/stage_probe
                 ;;
         tail)
-                run pytest_gpu_tail 900 python -u -m pytest tests -m gpu -x -v -k "fuzz or bench or multi_device or pinned_host or hip_failure or large_host" --timeout 300 --timeout-method thread
+                run pytest_gpu_tail 900 python -u -m pytest tests -m gpu -x -v -k "fuzz or bench or multi_device or pinned or hip_failure or large_host" --timeout 300 --timeout-method thread
                 ;;
         faulttests)
                 run pytest_gpu_fault 600 python -u -m pytest tests -m gpu -x -v -k "hip_failure or large_host_call or multi_device or pinned_host" --timeout 300 --timeout-method thread
