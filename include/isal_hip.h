@@ -186,16 +186,24 @@ void isal_hip_multi_partition(long long nstripes, int ndev, int dev, long long *
  * each call by where its shards live and how large it is:
  *   - any device-resident shard: the GPU kernels;
  *   - host-resident shards, (k + rows) * len > ISAL_HIP_CPU_MAX_BYTES: the GPU
- *     kernels through pinned / HBM staging;
- *   - host-resident shards up to ISAL_HIP_CPU_MAX_BYTES (default 8 MiB), or a
- *     host without a usable GPU: the engine's CPU route.
+ *     kernels. Page-locked host shards (hipHostMalloc / hipHostRegister) are
+ *     read and written in place through their device mapping (an update's
+ *     parity excepted: staged); pageable ones are staged through HBM, in
+ *     pipelined 4 MiB column chunks when longer (ISAL_HIP_CHUNK_KB,
+ *     ISAL_HIP_PIPE_CHUNKS=0 for one chunk, ISAL_HIP_PINNED_DIRECT=0 to stage
+ *     page-locked shards too). Large calls use a per-thread copy-out helper
+ *     thread and two extra streams;
+ *   - host-resident shards up to ISAL_HIP_CPU_MAX_BYTES (default 8 MiB; when
+ *     every shard is page-locked, ISAL_HIP_CPU_MAX_BYTES_PINNED, default
+ *     2 MiB), or a host without a usable GPU: the engine's CPU route.
  * ISAL_HIP_BACKEND=gpu forces the kernels for every call (and aborts when no
  * GPU is usable), =cpu sends every host-resident call to the CPU route,
  * =auto (default) is the rule above. Routing classifies each shard pointer
  * with hipPointerGetAttributes, so the HIP runtime is initialised on a host
- * with a GPU even under =cpu (device-resident shards still go to the GPU). If a HIP call fails during a
- * host-resident call, the call completes on the CPU route and the failure is
- * reported once on stderr; ISAL_HIP_LOG=1 logs every call's route.
+ * with a GPU even under =cpu (device-resident shards still go to the GPU).
+ * If a HIP call fails during a host-resident call, the call completes on the
+ * CPU route and the failure is reported once on stderr; ISAL_HIP_LOG=1 logs
+ * every call's route.
  * Environment knobs are read once; isal_hip_config_reload() re-reads them
  * (call it only while no other thread is inside the library).
  */

@@ -220,7 +220,7 @@ typedef struct outq {
         int quit, active;
         long long posted, handled; /* chunks launched / whose output copies are enqueued */
         /* the call being served */
-        int op, nsrc, nptr, len;
+        int nsrc, nptr, len;
         const uint64_t *view;
         unsigned char *const *dst;
         size_t chunk, slot, set_bytes;
@@ -914,7 +914,6 @@ gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsig
 
         q = c->oq;
         pthread_mutex_lock(&q->mu);
-        q->op = op;
         q->nsrc = nsrc;
         q->nptr = nptr;
         q->len = len;
