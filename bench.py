@@ -59,7 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--len", type=int, default=1 << 20, help="shard bytes")
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU per step")
     ap.add_argument("--workload", choices=["encode", "decode", "update", "encode-crc", "crc", "crc64", "encode-crc64",
-                                           "e2e-update", "e2e-encode"],
+                                           "e2e-update", "e2e-encode", "c1"],
                     default="encode",
                     help="e2e-*: host-resident (pinned) stripes streamed through the pipeline")
     ap.add_argument("--depth", type=int, default=3, help="e2e pipeline depth (stripes in flight)")
@@ -702,6 +702,8 @@ def main(argv=None):
         raise SystemExit("bench.py: --gpus must be >= 1")
     if (args.gpus or 1) > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args, argv)
+    if args.workload == "c1":
+        return c1_cpu(args)
     d = Dist(args.dry_run, args.dist_backend, args.dist_always, args.gpus)
     d.topology(args.dry_run)
     if args.dry_run:
@@ -1012,6 +1014,79 @@ def main(argv=None):
         print(json.dumps(result), flush=True)
     d.close()
     return 0
+
+
+def c1_cpu(args):
+    """BASELINE configs[0] (C1): k=4 p=2 Cauchy RS, one 64 KiB-shard stripe on
+    the CPU — the bit-exact plumbing case. Times the engine's drop-in
+    ec_encode_data on host buffers (a 384 KiB call: the engine's CPU route)
+    beside the reference's ec_encode_data_base (oracle/_ref/libisal_ref.so,
+    erasure_code/ec_base.c built from /root/reference; the same loop
+    erasure_code_base_perf.c times), both single-threaded, and checks that
+    both give the reference fixture's parity (FNV-1a of each row)."""
+    import numpy as np
+
+    import isal_amd
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import ecutil
+
+    k, p, n = 4, 2, 65536
+    case = ecutil.golden()["encode"][0]
+    assert (case["k"], case["rows"], case["len"], case["gen"]) == (k, p, n, "cauchy")
+    src = [ecutil.fill_bytes(n, case["seed"] + j) for j in range(k)]
+    a = isal_amd.gf_gen_cauchy1_matrix(k + p, k)
+    tbls = isal_amd.ec_init_tables(k, p, a[k * k:])
+    L = isal_amd.lib()
+    dst = [np.zeros(n, np.uint8) for _ in range(p)]
+    sp, dp, tp = isal_amd._pp(src), isal_amd._pp(dst), isal_amd._p(tbls)
+
+    def rate(fn):
+        fn()
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < min(args.cpu_seconds, 2.0) or reps < 10:
+            fn()
+            reps += 1
+        return (time.perf_counter() - t0) / reps
+
+    t_eng = rate(lambda: L.ec_encode_data(n, k, p, tp, sp, dp))
+    fnv = ecutil.oracle().fnv
+    ok_eng = [fnv(x) for x in dst] == case["fnv"]
+    ref = None
+    path = os.path.join(REPO, "oracle", "_ref", "libisal_ref.so")
+    if os.path.exists(path):
+        R = ctypes.CDLL(path)
+        u8p = ctypes.POINTER(ctypes.c_ubyte)
+        rt = np.zeros(32 * k * p, np.uint8)
+        R.ec_init_tables_base(k, p, a[k * k:].ctypes.data_as(u8p), rt.ctypes.data_as(u8p))
+        rdst = [np.zeros(n, np.uint8) for _ in range(p)]
+        rs, rd = isal_amd._pp(src), isal_amd._pp(rdst)
+        t_ref = rate(lambda: R.ec_encode_data_base(n, k, p, rt.ctypes.data_as(u8p), rs, rd))
+        ref = {"value": round((k + p) * n / t_ref / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "reference",
+               "sample": "ec_encode_data_base of the C1 stripe, erasure_code/ec_base.c built from /root/reference, "
+                         f"1 thread, {min(args.cpu_seconds, 2.0):.0f} s",
+               "parity_matches_fixture": [fnv(x) for x in rdst] == case["fnv"]}
+    result = {
+        "metric": "C1 ec_encode_data GiB/s on the host CPU (bit-exact plumbing, no GPU)",
+        "value": round((k + p) * n / t_eng / GIB, 4),
+        "unit": "GiB/s",
+        "n_gpus": 0,
+        "steps": None,
+        "warmup": 1,
+        "ms_per_step": round(t_eng * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "none",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "the reference fixture's C1 stripe (tests/golden/ec_base_golden.json encode[0])",
+        "config": {"workload": "C1: k=4 p=2 Cauchy RS (gf_gen_cauchy1_matrix), one stripe of 64 KiB shards, "
+                               "drop-in ec_encode_data on host buffers (engine CPU route)",
+                   "k": k, "p": p, "shard_bytes": n},
+        "parity_matches_fixture": ok_eng,
+        "cpu_baseline": ref,
+    }
+    print(json.dumps(result), flush=True)
+    return 0 if ok_eng else 1
 
 
 def e2e(args, d: Dist, a, k, p, n):

@@ -251,3 +251,20 @@ def test_reference_test_programs_on_cpu_route():
         assert v is not None, f"{name} not built"
         rc, out = v
         assert rc == 0 and "pass" in out.lower(), (name, out)
+
+
+def test_bench_c1_cpu_plumbing():
+    """BASELINE configs[0] (C1, k=4 p=2 Cauchy, one 64 KiB stripe on the CPU):
+    `bench.py --workload c1` times the drop-in call (engine CPU route) and the
+    reference's ec_encode_data_base, both == the fixture's parity."""
+    import json
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, os.path.join(ecutil.REPO, "bench.py"), "--workload", "c1",
+                        "--cpu-seconds", "0.2"], capture_output=True, text=True, timeout=300, cwd=ecutil.REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["parity_matches_fixture"] is True and out["value"] > 0
+    if out["cpu_baseline"] is not None:
+        assert out["cpu_baseline"]["parity_matches_fixture"] is True

@@ -250,6 +250,48 @@ def test_concurrent_callers(engine, oracle, gpu):
     assert not errors, errors
 
 
+def test_concurrent_large_host_callers(engine, oracle, gpu, monkeypatch):
+    """Large host calls from four threads at once, each thread with its own
+    staging sets, streams and copy-out worker: pipelined pageable calls
+    (several 64 KiB chunks), page-locked in-place calls and updates, every
+    result == oracle; the threads' workers are joined when the threads exit."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", "gpu")
+    _setenv(monkeypatch, "ISAL_HIP_CHUNK_KB", "64")
+    _setenv(monkeypatch, "ISAL_HIP_STAGE_MB", "8")
+    errors = []
+
+    def worker(t):
+        try:
+            for it in range(3):
+                k, rows, n = 4 + t, 2 + it, 800000 + 4096 * t + 16 * it  # > 4 MiB staged: chunked
+                coef = fill_bytes(k * rows, 1000 * t + it)
+                tbls = engine.ec_init_tables(k, rows, coef)
+                src = [fill_bytes(n, 70 * t + 11 * it + j) for j in range(k)]
+                if (t + it) % 2:  # page-locked sources and outputs: used in place
+                    src = [torch.from_numpy(x).pin_memory().numpy() for x in src]
+                    got = [torch.zeros(n, dtype=torch.uint8).pin_memory().numpy() for _ in range(rows)]
+                else:
+                    got = [np.zeros(n, np.uint8) for _ in range(rows)]
+                engine.ec_encode_data(n, k, rows, tbls, src, got)
+                want = oracle.encode(coef, k, rows, src)
+                if not all(np.array_equal(a, b) for a, b in zip(got, want)):
+                    errors.append(("encode", t, it))
+                upd = [np.zeros(n, np.uint8) for _ in range(rows)]
+                for v in range(k):
+                    engine.ec_encode_data_update(n, k, rows, v, tbls, src[v], upd)
+                if not all(np.array_equal(a, b) for a, b in zip(upd, want)):
+                    errors.append(("update", t, it))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errors, errors
+
+
 # --------------------------------------------------------------------------
 # batched extension + BASELINE.json configurations
 # --------------------------------------------------------------------------
