@@ -265,6 +265,9 @@ for s in $STEPS; do
                 run bench_c5 600 python bench.py --total-stripes 1048576 --steps 2 --warmup 1
                 cp "$OUT/bench_c5.log" "$OUT/bench_c5.json"
                 ;;
+        c1)
+                run bench_c1 120 python bench.py --workload c1
+                ;;
         zc)
                 run zc_probe 300 python tools/zc_probe.py
                 ;;
