@@ -406,7 +406,7 @@ stage_limit(void)
  * memory: 0 — it must be copied through a staging buffer. *is_dev tells
  * device memory (which no CPU route can read) from host memory. */
 static uint64_t
-classify(const void *p, int *is_dev)
+classify(const void *p, int dev, int *is_dev)
 {
         hipPointerAttribute_t a;
         hipError_t e;
@@ -423,10 +423,12 @@ classify(const void *p, int *is_dev)
                 *is_dev = 1;
                 return (uint64_t) (uintptr_t) p;
         }
-        if (a.type == hipMemoryTypeHost && a.devicePointer &&
+        if (a.type == hipMemoryTypeHost && a.devicePointer && a.device == dev &&
             isal_hip_knob(ISAL_HIP_KNOB_PINNED_DIRECT) != 0) {
                 /* attributes describe p itself (the mapping of the allocation
-                 * base plus p's offset into it) */
+                 * base plus p's offset into it). Only the mapping made for the
+                 * calling thread's device is used; page-locked memory of
+                 * another device is staged. */
                 return (uint64_t) (uintptr_t) a.devicePointer;
         }
         return 0;
@@ -1050,7 +1052,7 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         const int be = backend();
         const int nptr = nsrc + rows;
         uint64_t view_buf[512], *view;
-        int i, nstage = 0, ndev = 0, all_host;
+        int i, nstage = 0, ndev = 0, all_host, cur_dev;
         size_t bytes;
         gpu_res r;
         ctx_t *c;
@@ -1080,10 +1082,14 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 fprintf(stderr, "isal_hip: out of host memory\n");
                 abort();
         }
+        if (hipGetDevice(&cur_dev) != hipSuccess) {
+                (void) hipGetLastError();
+                cur_dev = -1; /* no page-locked shard is used in place */
+        }
         for (i = 0; i < nptr; i++) {
                 const void *p = i < nsrc ? src[i] : dst[i - nsrc];
                 int is_dev;
-                view[i] = classify(p, &is_dev);
+                view[i] = classify(p, cur_dev, &is_dev);
                 /* An update's parity in page-locked host memory is staged, not
                  * written in place: a kernel that failed after it started could
                  * have folded some of it already, and the CPU fallback could not
