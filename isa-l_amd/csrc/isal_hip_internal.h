@@ -115,6 +115,7 @@ enum {
         ISAL_HIP_KNOB_PIPE_CHUNKS,     /* 0: large host calls one chunk at a time (no copy overlap) */
         ISAL_HIP_KNOB_PINNED_DIRECT,   /* 0: stage page-locked host shards like pageable ones */
         ISAL_HIP_KNOB_CPU_MAX_BYTES_PINNED, /* auto route limit when every host shard is page-locked */
+        ISAL_HIP_KNOB_PAR_COPY,        /* 0: one thread issues a staged call's copies (no helper) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

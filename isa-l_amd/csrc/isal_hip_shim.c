@@ -206,6 +206,7 @@ typedef struct {
         hipEvent_t ev_in[PIPE_NBUF], ev_k[PIPE_NBUF], ev_out[PIPE_NBUF];
         int pipe_ready;
         struct outq *oq; /* the call thread's copy-out worker (gpu_pipelined) */
+        struct copyjob *jobs; /* [3]: worker's copies in / out, this thread's list */
 } ctx_t;
 
 /* Copy-out worker of a calling thread. The runtime serves a copy from or to
@@ -229,7 +230,30 @@ typedef struct outq {
         const char *what;
         long long fail_chunk;
         int rows_out;
+        /* a one-off batch of copies (gpu_chunked's second issuing thread) */
+        struct copyjob *job;
+        int job_state; /* 0 none, 1 posted, 2 finished */
 } outq_t;
+
+/* Copies the worker issues on s_out for gpu_chunked: after `after` (if set,
+ * a GPU-side wait), then `record` is recorded. */
+#define COPYJOB_MAX 512
+typedef struct copyjob {
+        int n;
+        struct {
+                void *dst;
+                const void *src;
+                size_t bytes;
+                hipMemcpyKind kind;
+        } cp[COPYJOB_MAX];
+        hipEvent_t after, record;
+        hipError_t err;
+        const char *what;
+} copyjob_t;
+
+static hipError_t outq_start(ctx_t *c);
+static void copyjob_post(outq_t *q, copyjob_t *j);
+static hipError_t copyjob_wait(outq_t *q, copyjob_t *j);
 
 static void outq_stop(ctx_t *c);
 
@@ -253,6 +277,7 @@ ctx_release(void *p)
                 (void) hipFree(c->d_stage);
         if (c->oq)
                 outq_stop(c);
+        free(c->jobs);
         if (c->pipe_ready) {
                 int b;
                 (void) hipStreamDestroy(c->s_in);
@@ -635,20 +660,64 @@ gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
         return r;
 }
 
+/* Issue this thread's share of a chunk's copies on the call's stream (the
+ * fault sites of the tests apply to them: an H2D list fails at its first
+ * copy, a D2H list at its second). *enq: copies enqueued. */
+static hipError_t
+issue_copies(ctx_t *c, const copyjob_t *j, int fault_site, long long ci, const char **what, int *enq)
+{
+        int i;
+        hipError_t e;
+        *enq = 0;
+        for (i = 0; i < j->n; i++) {
+                e = fault_at(i == 1 || fault_site == FAULT_H2D ? fault_site : FAULT_NONE, ci)
+                            ? hipErrorOutOfMemory
+                            : hipMemcpyAsync(j->cp[i].dst, j->cp[i].src, j->cp[i].bytes, j->cp[i].kind,
+                                             c->stream);
+                if (e != hipSuccess) {
+                        *what = j->cp[i].kind == hipMemcpyHostToDevice ? "hipMemcpyAsync(H2D chunk)"
+                                                                        : "hipMemcpyAsync(D2H chunk)";
+                        return e;
+                }
+                *enq = i + 1;
+        }
+        return hipSuccess;
+}
+
+static void
+job_add(copyjob_t *j, void *dst, const void *src, size_t bytes, hipMemcpyKind kind)
+{
+        j->cp[j->n].dst = dst;
+        j->cp[j->n].src = src;
+        j->cp[j->n].bytes = bytes;
+        j->cp[j->n].kind = kind;
+        j->n++;
+}
+
 /* Column-chunked mode: whole shards when nothing is staged, else chunks of at
  * most stage_limit() bytes over all staged shards. r.done advances past every
- * chunk whose outputs are final. */
+ * chunk whose outputs are final.
+ * With two or more staged shards the chunk's copies are shared with the
+ * calling thread's worker (ISAL_HIP_PAR_COPY=0: not): a pageable copy runs
+ * synchronously on the thread that issues it with a fixed cost of ~14 us,
+ * and a second issuing thread hides part of it (H2D of 2 MiB shards:
+ * 36 -> 41 GB/s, profiles/r03_stage_probe_b.jsonl). The worker copies in on
+ * s_out (the kernel waits for its event); for an encode it also copies half
+ * the parity out after the kernel. An update's parity comes back from this
+ * thread alone, in row order, so a failure leaves a known prefix of rows
+ * updated (rows_out). */
 static gpu_res
 gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
             unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
             int nstage)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
-        int nptr = nsrc + rows, i, nslots;
+        int nptr = nsrc + rows, i, nslots, par = 0;
         size_t chunk, slot;
         layout_t L;
         uint64_t *h_ptrs;
         long long c0;
+        copyjob_t *win = NULL, *wout = NULL, *mine = NULL;
 
         if (nstage) {
                 size_t per = stage_limit() / (size_t) nstage;
@@ -662,6 +731,18 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                 chunk = (size_t) len;
                 slot = 0;
         }
+        if (nstage >= 2 && nptr <= COPYJOB_MAX && isal_hip_knob(ISAL_HIP_KNOB_PAR_COPY) != 0) {
+                if (!c->jobs)
+                        c->jobs = (copyjob_t *) malloc(3 * sizeof(copyjob_t));
+                /* no helper (no memory, no thread): one issuing thread, as before */
+                par = c->jobs && ensure_pipe(c) == hipSuccess && outq_start(c) == hipSuccess;
+                (void) hipGetLastError();
+                if (par) {
+                        win = &c->jobs[0];
+                        wout = &c->jobs[1];
+                        mine = &c->jobs[2];
+                }
+        }
 
         L = call_layout(op, len, k, rows, nptr, 0);
         GPU_TRY(r, ensure_args(c, L.stage_off));
@@ -670,8 +751,13 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
 
         for (c0 = 0; c0 < len; c0 += (long long) chunk) {
                 int clen = (int) ((long long) len - c0 < (long long) chunk ? len - c0 : (long long) chunk);
-                int s = 0, vec16 = 1;
+                int s = 0, vec16 = 1, nin = 0, enq = 0;
                 const long long ci = c0 / (long long) chunk;
+                if (par) {
+                        win->n = mine->n = 0;
+                        win->after = NULL;
+                        win->record = c->ev_in[0];
+                }
                 for (i = 0; i < nptr; i++) {
                         unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
                         uint64_t d;
@@ -682,13 +768,38 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                                 d = (uint64_t) (uintptr_t) st;
                                 /* sources, and outputs of a read-modify-write update or
                                  * of a verify, go in */
-                                if (i < nsrc || op != OP_ENCODE)
-                                        GPU_TRY_ATC(r, FAULT_H2D, ci, hipMemcpyAsync(st, host + c0, (size_t) clen,
-                                                                  hipMemcpyHostToDevice, c->stream));
+                                if (i < nsrc || op != OP_ENCODE) {
+                                        if (!par)
+                                                GPU_TRY_ATC(r, FAULT_H2D, ci,
+                                                            hipMemcpyAsync(st, host + c0, (size_t) clen,
+                                                                           hipMemcpyHostToDevice, c->stream));
+                                        else
+                                                job_add(nin++ & 1 ? win : mine, st, host + c0, (size_t) clen,
+                                                        hipMemcpyHostToDevice);
+                                }
                         }
                         h_ptrs[i] = d;
                         if (d & 15)
                                 vec16 = 0;
+                }
+                if (par) {
+                        hipError_t e, ew;
+                        const char *what = NULL;
+                        if (win->n)
+                                copyjob_post(c->oq, win);
+                        e = issue_copies(c, mine, FAULT_H2D, ci, &what, &enq);
+                        ew = win->n ? copyjob_wait(c->oq, win) : hipSuccess;
+                        if (e == hipSuccess && ew != hipSuccess) {
+                                e = ew;
+                                what = win->what;
+                        }
+                        if (e == hipSuccess && win->n)
+                                e = hipStreamWaitEvent(c->stream, c->ev_in[0], 0);
+                        if (e != hipSuccess) {
+                                r.err = e;
+                                r.what = what ? what : "hipStreamWaitEvent(helper copies in)";
+                                return r;
+                        }
                 }
                 GPU_TRY(r, hipMemcpyAsync(c->d_args, c->h_args, L.args_bytes,
                                           hipMemcpyHostToDevice, c->stream));
@@ -711,18 +822,56 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                 s = 0; /* staged slots are in pointer order: outputs follow sources */
                 r.chunk_end = c0 + clen;
                 r.rows_out = 0;
-                for (i = 0; i < nptr; i++) {
-                        if (view[i])
-                                continue;
-                        if (i >= nsrc) {
-                                GPU_TRY_ATC(r, i - nsrc == 1 ? FAULT_D2H : FAULT_NONE, ci,
-                                           hipMemcpyAsync(dst[i - nsrc] + c0,
-                                                          c->d_stage + (size_t) s * slot,
-                                                          (size_t) clen, hipMemcpyDeviceToHost,
-                                                          c->stream));
-                                r.rows_out = i - nsrc + 1;
+                if (par && op == OP_ENCODE) {
+                        /* encode: half the parity rows leave through the worker */
+                        hipError_t e, ew;
+                        const char *what = NULL;
+                        int nout = 0;
+                        wout->n = mine->n = 0;
+                        wout->after = c->ev_k[0];
+                        wout->record = c->ev_out[0];
+                        GPU_TRY(r, hipEventRecord(c->ev_k[0], c->stream));
+                        for (i = 0; i < nptr; i++) {
+                                if (view[i])
+                                        continue;
+                                if (i >= nsrc)
+                                        job_add(nout++ & 1 ? wout : mine, dst[i - nsrc] + c0,
+                                                c->d_stage + (size_t) s * slot, (size_t) clen,
+                                                hipMemcpyDeviceToHost);
+                                s++;
                         }
-                        s++;
+                        if (wout->n)
+                                copyjob_post(c->oq, wout);
+                        e = issue_copies(c, mine, FAULT_D2H, ci, &what, &enq);
+                        ew = wout->n ? copyjob_wait(c->oq, wout) : hipSuccess;
+                        /* some parity copies may be under way: a failed drain must abort */
+                        r.rows_out = enq || wout->n ? 1 : 0;
+                        if (e == hipSuccess && ew != hipSuccess) {
+                                e = ew;
+                                what = wout->what;
+                        }
+                        if (e == hipSuccess && wout->n)
+                                e = fault_at(FAULT_SYNC, ci) ? hipErrorOutOfMemory
+                                                             : hipStreamSynchronize(c->s_out);
+                        if (e != hipSuccess) {
+                                r.err = e;
+                                r.what = what ? what : "hipStreamSynchronize(helper copies out)";
+                                return r;
+                        }
+                } else {
+                        for (i = 0; i < nptr; i++) {
+                                if (view[i])
+                                        continue;
+                                if (i >= nsrc) {
+                                        GPU_TRY_ATC(r, i - nsrc == 1 ? FAULT_D2H : FAULT_NONE, ci,
+                                                    hipMemcpyAsync(dst[i - nsrc] + c0,
+                                                                   c->d_stage + (size_t) s * slot,
+                                                                   (size_t) clen, hipMemcpyDeviceToHost,
+                                                                   c->stream));
+                                        r.rows_out = i - nsrc + 1;
+                                }
+                                s++;
+                        }
                 }
                 GPU_TRY_ATC(r, FAULT_SYNC, ci, hipStreamSynchronize(c->stream));
                 r.done = c0 + clen;
@@ -783,6 +932,50 @@ copy_out_chunk(ctx_t *c, const outq_t *q, long long ci, const char **what, int *
         return e;
 }
 
+static void
+run_copyjob(ctx_t *c, copyjob_t *j)
+{
+        int i;
+        j->err = hipSuccess;
+        j->what = NULL;
+        if (j->after && (j->err = hipStreamWaitEvent(c->s_out, j->after, 0)) != hipSuccess) {
+                j->what = "hipStreamWaitEvent(helper copies)";
+                return;
+        }
+        for (i = 0; i < j->n; i++)
+                if ((j->err = hipMemcpyAsync(j->cp[i].dst, j->cp[i].src, j->cp[i].bytes, j->cp[i].kind,
+                                             c->s_out)) != hipSuccess) {
+                        j->what = "hipMemcpyAsync(helper copies)";
+                        return;
+                }
+        if (j->record && (j->err = hipEventRecord(j->record, c->s_out)) != hipSuccess)
+                j->what = "hipEventRecord(helper copies)";
+}
+
+static void
+copyjob_post(outq_t *q, copyjob_t *j)
+{
+        pthread_mutex_lock(&q->mu);
+        q->job = j;
+        q->job_state = 1;
+        pthread_cond_broadcast(&q->cv);
+        pthread_mutex_unlock(&q->mu);
+}
+
+/* Wait until the worker has issued the posted job's copies (pageable ones
+ * are complete by then); its error. */
+static hipError_t
+copyjob_wait(outq_t *q, copyjob_t *j)
+{
+        pthread_mutex_lock(&q->mu);
+        while (q->job_state == 1)
+                pthread_cond_wait(&q->cv, &q->mu);
+        q->job_state = 0;
+        q->job = NULL;
+        pthread_mutex_unlock(&q->mu);
+        return j->err;
+}
+
 static void *
 outq_main(void *arg)
 {
@@ -795,10 +988,20 @@ outq_main(void *arg)
                 const char *what = NULL;
                 int rows_out;
                 hipError_t e;
-                while (!q->quit && !(q->active && q->err == hipSuccess && q->handled < q->posted))
+                while (!q->quit && q->job_state != 1 &&
+                       !(q->active && q->err == hipSuccess && q->handled < q->posted))
                         pthread_cond_wait(&q->cv, &q->mu);
                 if (q->quit)
                         break;
+                if (q->job_state == 1) {
+                        copyjob_t *j = q->job;
+                        pthread_mutex_unlock(&q->mu);
+                        run_copyjob(c, j);
+                        pthread_mutex_lock(&q->mu);
+                        q->job_state = 2;
+                        pthread_cond_broadcast(&q->cv);
+                        continue;
+                }
                 ci = q->handled;
                 pthread_mutex_unlock(&q->mu);
                 e = copy_out_chunk(c, q, ci, &what, &rows_out);

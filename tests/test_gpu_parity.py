@@ -428,7 +428,7 @@ def test_hip_failure_falls_back_to_cpu_route(engine, oracle, gpu, monkeypatch, s
             assert engine.fallbacks() > before, (site, n)
 
 
-@pytest.mark.parametrize("piped", ["1", "0"])
+@pytest.mark.parametrize("piped", ["1", "0", "seq"])
 @pytest.mark.parametrize("site", [2, 3, 4, 5])
 def test_hip_failure_in_a_later_chunk_resumes_on_cpu(engine, oracle, gpu, monkeypatch, site, piped):
     """A HIP failure in column chunk 3 of a call (ISAL_HIP_FAULT_CHUNK): chunks
@@ -442,7 +442,10 @@ def test_hip_failure_in_a_later_chunk_resumes_on_cpu(engine, oracle, gpu, monkey
     _setenv(monkeypatch, "ISAL_HIP_CPU_MAX_BYTES", "0")
     _setenv(monkeypatch, "ISAL_HIP_STAGE_MB", "1")
     _setenv(monkeypatch, "ISAL_HIP_CHUNK_KB", "64")
-    _setenv(monkeypatch, "ISAL_HIP_PIPE_CHUNKS", piped)
+    # "1": pipelined chunks; "0": one chunk at a time, copies shared with the
+    # helper thread; "seq": one chunk at a time, one issuing thread
+    _setenv(monkeypatch, "ISAL_HIP_PIPE_CHUNKS", "1" if piped == "1" else "0")
+    _setenv(monkeypatch, "ISAL_HIP_PAR_COPY", "0" if piped == "seq" else "1")
     _setenv(monkeypatch, "ISAL_HIP_FAULT", str(site))
     _setenv(monkeypatch, "ISAL_HIP_FAULT_CHUNK", "3")
     rng = np.random.default_rng(site)

@@ -61,6 +61,9 @@ def main():
         row["gpu_pinned_gb_s"] = round((k + p) * n / row["gpu_pinned_us"] / 1e3, 2)
         if n >= 1 << 20:  # the chunked route: pipelined (default) vs one chunk at a time
             row["gpu_unpipelined_us"] = round(per_call(k, p, n, "gpu", piped="0"), 1)
+            os.environ["ISAL_HIP_PAR_COPY"] = "0"  # one thread issues every copy (round-2 behaviour)
+            row["gpu_one_thread_us"] = round(per_call(k, p, n, "gpu", piped="0"), 1)
+            os.environ["ISAL_HIP_PAR_COPY"] = ""
             row["gpu_gb_s"] = round((k + p) * n / gpu / 1e3, 2)
         if pinned_crossover is None and cpu is not None and row["gpu_pinned_us"] < cpu:
             pinned_crossover = (k + p) * n
