@@ -241,6 +241,12 @@ for s in $STEPS; do
         probe)
                 run probe 300 isa-l_amd/build/ec_probe
                 ;;
+        valu)
+                # issue rate of v_perm / v_bitop3 / SDWA shifts vs v_add, random ds_read_b64 (tools/valu_probe.hip)
+                for w in 2 4 8; do
+                        run valu_probe_w$w 120 tools/valu_probe $w
+                done
+                ;;
         refcpu)
                 # the reference's own perf harnesses on the host cores (no GPU)
                 run refcpu_encode 200 python3 tools/cpu_ref_baseline.py --which encode
