@@ -801,18 +801,21 @@ def main(argv=None):
             bytes_per_launch = (k + p) * n * S
             u = enc_group(k)
             reg = k == u and os.environ.get("ISAL_HIP_CRC64_SRC_CHAIN") == "reg"
-            # chunk path: 0 field tables, 1 slicing-by-8 byte tables (default), 2 hybrid
-            # byte/field tables (experiment, load group 10 only)
-            sl = {"0": 0, "2": 2}.get(os.environ.get("ISAL_HIP_CRC64_SLICE", "1"), 1)
-            if sl == 2 and (u != 10 or reg):
+            # chunk path: 0 field tables, 1 slicing-by-8 byte tables, 2 hybrid byte/field
+            # tables (experiment), 3 byte tables pipelined into the GF rows (default;
+            # 2 and 3 for load group 10 only, 3 for p <= 4; elsewhere 1)
+            sl = {"0": 0, "1": 1, "2": 2}.get(os.environ.get("ISAL_HIP_CRC64_SLICE", "3"), 3)
+            if sl in (2, 3) and (u != 10 or reg or (sl == 3 and p > 4)):
                 sl = 1
             # lane groups per workgroup: the launcher's rule (crc64_kernels.hip fused_nv)
-            tabs_b, la_b, cap = {0: 2688, 1: 4096, 2: 1024}[sl] * 8, k * 256 * 8, 160 * 1024
+            tabs_b, la_b, cap = {0: 2688, 1: 4096, 2: 1024, 3: 4096}[sl] * 8, k * 256 * 8, 160 * 1024
             nv_env = os.environ.get("ISAL_HIP_CRC64_FUSED_NV")
             if reg or tabs_b + 2 * la_b >= cap:
                 nv = 1
             elif nv_env in ("1", "2"):
                 nv = int(nv_env)
+            elif sl == 3:
+                nv = 1
             else:
                 nv = 2 if 2 * (cap // (tabs_b + 2 * la_b)) > cap // (tabs_b + la_b) else 1
             # X0: Vandermonde row 0 derived
@@ -996,7 +999,7 @@ def main(argv=None):
                 port_check = (data[0].cpu().numpy(), out[0].cpu().numpy()) if args.workload == "encode" else None
                 for key, ring in (("cpu_baseline_simd_port", 1), ("cpu_baseline_simd_port_cold", args.cold_ring)):
                     result[key] = cpu_baseline(k, rows, n, min(args.cpu_seconds, 5.0), threads,
-                                               port_check if ring == 1 else None, impl="gfni", ring=ring)
+                                               port_check, impl="gfni", ring=ring)
         else:
             check = None
             if args.workload in ("encode-crc", "encode-crc64"):

@@ -561,6 +561,157 @@ __device__ __forceinline__ uint64_t chain_step_sl(const uint64_t* lt, uint64_t b
   return c.get();
 }
 
+// ---- SL 3: the byte-table chain steps software-pipelined with the GF rows --
+// In the SL 1 kernel the compiler emits each chain step as pairs of
+// ds_read_b64 with an s_waitcnt after every pair (the byte tables conflict, so
+// each wait is a full LDS round trip), after the pair's GF work: the wave
+// stalls on LDS while it holds VALU work it could issue. Here a source pair's
+// region is cut into stages by scheduling barriers, and each stage issues a
+// chain's eight lookups of one half-step, then runs one GF row (~38 VALU) of
+// independent work before folding them:
+//   S   chain states of sources a, b from LDS; selectors; row 0 (masked XOR)
+//       (the previous pair's b: fold -> its state); R1a: a's first 8 bytes
+//   row r1 | F1a fold, R2a: a's last 8 bytes
+//   row r2 | F2a fold -> a's state; R1b
+//   row r3 (+ any further rows) | F1b fold, R2b (finished by the next pair)
+// Same tables, same arithmetic as chain_step_sl<PH, 1>.
+struct Look8 {
+  uint64_t v[8];
+};
+
+// The lookups are volatile LDS loads: a plain load is placed next to its use
+// by instruction selection, before the scheduling barriers are seen, which
+// would undo the stages; volatile accesses keep their order against the barriers.
+__device__ __forceinline__ uint64_t tab8_issue(const uint64_t* t, int j, uint32_t o) {
+  typedef const __attribute__((address_space(3))) char lchar;
+  typedef const volatile __attribute__((address_space(3))) uint64_t lu64;
+  return *(lu64*)((lchar*)(t) + j * 2048 + o);
+}
+
+__device__ __forceinline__ void issue8(Look8& r, const uint64_t* t, uint32_t lo, uint32_t hi) {
+  uint32_t o[4], q[4];
+  byte_offs8(lo, o);
+  byte_offs8(hi, q);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r.v[i] = tab8_issue(t, i, o[i]);
+    r.v[4 + i] = tab8_issue(t, 4 + i, q[i]);
+  }
+}
+
+__device__ __forceinline__ X64 fold8(const Look8& r) {
+  X64 a{0u, 0u};
+  a.add2(r.v[0], r.v[1]);
+  a.add2(r.v[2], r.v[3]);
+  a.add2(r.v[4], r.v[5]);
+  a.add2(r.v[6], r.v[7]);
+  return a;
+}
+
+// acc[l] ^= c[l][a] * x ^ c[l][b] * y for rows [L0, L1) (selectors and
+// coefficient tables already in registers).
+template <int P, int L0, int L1>
+__device__ __forceinline__ void mac_rows2(uint32_t (&acc)[P][4], const Sel (&sx)[4], const Sel (&sy)[4],
+                                          const Coef (&ca)[P], const Coef (&cb)[P]) {
+#pragma unroll
+  for (int l = L0; l < L1; ++l) {
+    const Coef& a = ca[l];
+    const Coef& b = cb[l];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t v = acc[l][d];
+      v = xor3(v, __builtin_amdgcn_perm(a.a1, a.a0, sx[d].s0), __builtin_amdgcn_perm(a.b1, a.b0, sx[d].s1));
+      v = xor3(v, __builtin_amdgcn_perm(0u, a.c, sx[d].s2), __builtin_amdgcn_perm(b.a1, b.a0, sy[d].s0));
+      v = xor3(v, __builtin_amdgcn_perm(b.b1, b.b0, sy[d].s1), __builtin_amdgcn_perm(0u, b.c, sy[d].s2));
+      acc[l][d] = v;
+    }
+  }
+}
+
+// The coefficient tables come in by scalar loads, which share lgkmcnt with
+// the LDS lookups and may complete out of order: a wait for one of them is a
+// wait for every lookup in flight. So a pair's tables are loaded and waited
+// for in its first stage, behind the fold that waits anyway.
+template <int P, int L0>
+__device__ __forceinline__ void load_coefs(Coef (&c)[P], const uint32_t* __restrict__ t) {
+#pragma unroll
+  for (int l = L0; l < P; ++l) c[l] = load_coef(t + l * kTbl);
+}
+
+template <int P, int L0>
+__device__ __forceinline__ void have_coefs(const Coef (&c)[P]) {
+#pragma unroll
+  for (int l = L0; l < P; ++l)
+    asm volatile("" ::"s"(c[l].a0), "s"(c[l].a1), "s"(c[l].b0), "s"(c[l].b1), "s"(c[l].c));
+}
+
+// One source pair; `car` holds the previous pair's second chain, its last
+// eight lookups in flight (cp = where its state goes; nullptr: none).
+template <int P, bool R0, int PH>
+__device__ __forceinline__ void mac_feed_pair_pipe(uint32_t (&acc)[P][4], const uint4& x, const uint4& y,
+                                                   const uint32_t* __restrict__ tx,
+                                                   const uint32_t* __restrict__ ty, uint32_t mx,
+                                                   uint32_t my, uint64_t* pa, uint64_t* pb,
+                                                   const uint64_t* lt, Look8& car, uint64_t*& cp) {
+  constexpr int R = P - (R0 ? 1 : 0);  // rows through the GF lookups
+  constexpr int B1 = R0 ? 1 : 0, B2 = B1 + (R + 2) / 3, B3 = B2 + (R + 1) / 3;
+  const uint64_t* t2 = lt + (PH == 1 ? kSA : kSB);
+  const uint64_t sa = *pa, sb = *pb;
+  const Sel sx[4] = {split(x.x), split(x.y), split(x.z), split(x.w)};
+  const Sel sy[4] = {split(y.x), split(y.y), split(y.z), split(y.w)};
+  if constexpr (R0) {
+    acc[0][0] = xor_and(xor_and(acc[0][0], x.x, mx), y.x, my);
+    acc[0][1] = xor_and(xor_and(acc[0][1], x.y, mx), y.y, my);
+    acc[0][2] = xor_and(xor_and(acc[0][2], x.z, mx), y.z, my);
+    acc[0][3] = xor_and(xor_and(acc[0][3], x.w, mx), y.w, my);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (cp) *cp = fold8(car).get();
+  Coef ca[P], cb[P];
+  load_coefs<P, B1>(ca, tx);
+  load_coefs<P, B1>(cb, ty);
+  have_coefs<P, B1>(ca);
+  have_coefs<P, B1>(cb);
+  __builtin_amdgcn_sched_barrier(0);
+  issue8(car, lt + kSA, x.x ^ static_cast<uint32_t>(sa), x.y ^ static_cast<uint32_t>(sa >> 32));
+  __builtin_amdgcn_sched_barrier(0);
+  mac_rows2<P, B1, B2>(acc, sx, sy, ca, cb);
+  __builtin_amdgcn_sched_barrier(0);
+  const X64 ua = fold8(car);
+  issue8(car, t2, x.z ^ ua.lo, x.w ^ ua.hi);
+  __builtin_amdgcn_sched_barrier(0);
+  mac_rows2<P, B2, B3>(acc, sx, sy, ca, cb);
+  __builtin_amdgcn_sched_barrier(0);
+  *pa = fold8(car).get();
+  issue8(car, lt + kSA, y.x ^ static_cast<uint32_t>(sb), y.y ^ static_cast<uint32_t>(sb >> 32));
+  __builtin_amdgcn_sched_barrier(0);
+  mac_rows2<P, B3, P>(acc, sx, sy, ca, cb);
+  __builtin_amdgcn_sched_barrier(0);
+  const X64 ub = fold8(car);
+  issue8(car, t2, y.z ^ ub.lo, y.w ^ ub.hi);
+  cp = pb;
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// U sources j..j+U-1 (U even, P <= 4) with LDS chain states at la (row stride
+// kLa): one chain's eight lookups in flight at a time, the last pair's second
+// chain finishing behind the next pair's selectors and row 0.
+template <int P, int U, bool R0, int PH>
+__device__ __forceinline__ void mac_feed_pipe(uint32_t (&acc)[P][4], const uint4 (&x)[U], int j,
+                                              const uint32_t* __restrict__ tbl, uint64_t* la, int kLa,
+                                              const uint64_t* lt, unsigned long long x0src) {
+  static_assert(U % 2 == 0 && P <= 4, "pairs of sources, tables of both in SGPRs");
+  Look8 car;
+  uint64_t* cp = nullptr;
+#pragma unroll
+  for (int u = 0; u < U; u += 2)
+    mac_feed_pair_pipe<P, R0, PH>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl,
+                                  tbl + (j + u + 1) * P * kTbl, r0_mask(x0src, j + u),
+                                  r0_mask(x0src, j + u + 1), la + (j + u) * kLa,
+                                  la + (j + u + 1) * kLa, lt, car, cp);
+  *cp = fold8(car).get();
+}
+
 template <int P, int U, bool REG>
 constexpr int fused64_waves() {
   constexpr int est = (4 * U * (REG ? 2 : 1) + 6 * P + (REG ? 2 * U : 0) + 88 + 7) / 8 * 8;
@@ -691,7 +842,11 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
             for (; j + U <= k; j += U) {
               uint4 x[U];
               load_grp<U>(x, sp, j, off, len);
-              mac_feed<P, U, X0>(acc, x, j, tbl + z, feed, x0src);
+              if constexpr (SL == 3)
+                mac_feed_pipe<P, U, X0, decltype(phc)::value>(acc, x, j, tbl + z, la + threadIdx.x, kLa,
+                                                              lt, x0src);
+              else
+                mac_feed<P, U, X0>(acc, x, j, tbl + z, feed, x0src);
             }
             for (; j < k; ++j) {
               uint4 x[1];
@@ -774,10 +929,13 @@ bool src_chain_reg64() {
 // lane groups: 4.58 -> 4.01 ms (VALU 2.40e9 -> 1.83e9 wave-instructions,
 // profiles/r02_fastcrc_*); with register chains (240 VGPRs) it is slower.
 // 0: field tables, 1: byte (slicing) tables, 2: hybrid tables (experiment,
-// instantiated for the C2 load group U = 10 only; other U use byte tables).
+// instantiated for the C2 load group U = 10 only; other U use byte tables),
+// 3 (the default; byte tables elsewhere): byte tables with the chain steps
+// pipelined into the GF rows, for load group U = 10 and P <= 4 — C2 step
+// 3.386 -> 3.305 ms (profiles/r03_pipe64_benches.jsonl).
 int slice64() {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_SLICE);
-  return v == 0 ? 0 : v == 2 ? 2 : 1;
+  return v == 0 ? 0 : v == 1 ? 1 : v == 2 ? 2 : 3;
 }
 
 // 256-lane groups per workgroup of the LDS-chain fused kernel: the knob
@@ -790,6 +948,9 @@ int fused_nv(int sl, int k) {
                la = static_cast<size_t>(k) * kBlock * 8;
   if (tabs + 2 * la >= cap) return 1;  // leave LDS headroom: never the whole 160 KiB
   if (v == 1 || v == 2) return static_cast<int>(v);
+  // the pipelined path holds 140 VGPRs (3 waves/SIMD): a 512-lane workgroup
+  // (8 waves) would leave one workgroup, 2 waves/SIMD, per CU
+  if (sl == 3) return 1;
   return 2 * (cap / (tabs + 2 * la)) > cap / (tabs + la) ? 2 : 1;
 }
 
@@ -811,13 +972,17 @@ void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_
   const size_t lds = static_cast<size_t>(k) * kBlock * 8;
   const bool reg = k == U && src_chain_reg64();
   int sl = slice64();
-  if (sl == 2 && (U != 10 || reg)) sl = 1;
+  if ((sl == 2 || sl == 3) && (U != 10 || reg || P > 4)) sl = 1;
   const bool nv2 = !reg && fused_nv(sl, k) == 2;
   if (reg) {
     if (sl) FUSED64_X0(true, 1, 1); else FUSED64_X0(true, 0, 1);
   } else if (sl == 2) {
     if constexpr (U == 10) {
       if (nv2) FUSED64_X0(false, 2, 2); else FUSED64_X0(false, 2, 1);
+    }
+  } else if (sl == 3) {
+    if constexpr (U == 10 && P <= 4) {
+      if (nv2) FUSED64_X0(false, 3, 2); else FUSED64_X0(false, 3, 1);
     }
   } else if (sl) {
     if (nv2) FUSED64_X0(false, 1, 2); else FUSED64_X0(false, 1, 1);

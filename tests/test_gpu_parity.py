@@ -396,6 +396,67 @@ def test_config_c2_c3_full_size(engine, oracle, gpu):
     dec.close()
 
 
+@pytest.mark.parametrize("k,rows", [(223, 32), (250, 5), (128, 127), (1, 254)])
+def test_maximum_stripe_width_vs_oracle(engine, oracle, gpu, k, rows):
+    """The widest stripes GF(2^8) allows (k + rows <= 255; the reference's
+    erasure_code_test.c runs up to 127 sources, gf_vect_dot_prod_base_test.c
+    250): device shards through the drop-in call (several kernel passes of
+    rows, every source in each), ragged length, byte for byte vs the oracle."""
+    import torch
+
+    n = 4096 * 3 + 13
+    coef = fill_bytes(k * rows, 77 + k)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    src = [fill_bytes(n, 900 + j) for j in range(k)]
+    want = oracle.encode(coef, k, rows, src)
+    dsrc = [_dev(torch, s, gpu) for s in src]
+    dout = [torch.zeros(n, dtype=torch.uint8, device=gpu) for _ in range(rows)]
+    launches = engine.kernel_launches()
+    engine.ec_encode_data(n, k, rows, tbls, dsrc, dout)
+    assert engine.kernel_launches() > launches
+    for l in range(rows):
+        assert np.array_equal(_host(dout[l]), want[l]), l
+    # update path at the same width: fold the sources in one at a time
+    for d in dout:
+        d.zero_()
+    for v in range(k):
+        engine.ec_encode_data_update(n, k, rows, v, tbls, dsrc[v], dout)
+    for l in range(rows):
+        assert np.array_equal(_host(dout[l]), want[l]), ("update", l)
+
+
+def test_maximum_shard_length(engine, gpu):
+    """len = INT_MAX (2^31 - 1 bytes, the largest `int len` the API takes):
+    32-bit buffer offsets and the ragged last tile at the top of the range.
+    Checked through size-independent properties: row 0 of the Vandermonde
+    matrix is all ones, so parity 0 == XOR of the sources (torch, exact);
+    row 1 at 2^20 sampled byte positions plus the first and last 64 KiB ==
+    the GF(2^8) product table (built from gf_mul); the 65 guard bytes after
+    every shard stay untouched."""
+    import torch
+
+    if torch.cuda.get_device_properties(gpu).total_memory < 64 << 30:
+        pytest.skip("needs a large-HBM GPU")
+    k, rows, n, guard = 2, 2, (1 << 31) - 1, 65  # rows start 16-byte aligned
+    a = engine.gf_gen_rs_matrix(k + rows, k)
+    tbls = engine.ec_init_tables(k, rows, a[k * k:])
+    g = torch.Generator(device=gpu).manual_seed(31)
+    src = torch.empty((k, n + guard), dtype=torch.uint8, device=gpu)
+    src.random_(generator=g)
+    out = torch.full((rows, n + guard), 0xA5, dtype=torch.uint8, device=gpu)
+    engine.ec_encode_data(n, k, rows, tbls, [src[j] for j in range(k)], [out[l] for l in range(rows)])
+    torch.cuda.synchronize()
+    assert torch.equal(out[0, :n], src[0, :n] ^ src[1, :n])
+    assert bool((out[:, n:] == 0xA5).all())
+    mul = torch.tensor([[engine.gf_mul(c, x) for x in range(256)] for c in range(256)],
+                       dtype=torch.uint8, device=gpu)
+    c0, c1 = int(a[(k + 1) * k]), int(a[(k + 1) * k + 1])
+    pos = torch.cat([torch.arange(0, 1 << 16, device=gpu), torch.arange(n - (1 << 16), n, device=gpu),
+                     torch.randint(0, n, (1 << 20,), generator=g, device=gpu)])
+    s0, s1 = src[0, pos].long(), src[1, pos].long()
+    assert torch.equal(out[1, pos], mul[c0][s0] ^ mul[c1][s1])
+
+
 @pytest.mark.parametrize("site", [1, 2, 3, 4, 5])
 def test_hip_failure_falls_back_to_cpu_route(engine, oracle, gpu, monkeypatch, site):
     """SURVEY §5 'never fail where the reference succeeds': ISAL_HIP_FAULT makes
@@ -1067,7 +1128,8 @@ def test_encode_crc64_knobs(engine, oracle, gpu, monkeypatch, pair, chain, k, ro
 @pytest.mark.parametrize("slice_,pair,chain,nv", [
     ("1", 1, "lds", 1), ("1", 0, "lds", 1), ("1", 1, "reg", 1), ("1", 0, "reg", 1),
     ("1", 1, "lds", 2), ("1", 0, "lds", 2), ("0", 1, "lds", 2), ("0", 0, "lds", 2),
-    ("0", 1, "lds", 1), ("0", 1, "reg", 1), ("2", 1, "lds", 1), ("2", 1, "lds", 2), ("2", 0, "lds", 2)])
+    ("0", 1, "lds", 1), ("0", 1, "reg", 1), ("2", 1, "lds", 1), ("2", 1, "lds", 2), ("2", 0, "lds", 2),
+    ("3", 1, "lds", 1), ("3", 1, "lds", 2), ("3", 0, "lds", 2)])
 @pytest.mark.parametrize("k,rows,n,ns,skew,tt,variant", ENCODE_CRC64_SHAPES[:5])
 def test_encode_crc64_slice_knobs(engine, oracle, gpu, monkeypatch, slice_, pair, chain, nv, k, rows, n,
                                   ns, skew, tt, variant):
@@ -1082,16 +1144,33 @@ def test_encode_crc64_slice_knobs(engine, oracle, gpu, monkeypatch, slice_, pair
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant)
 
 
-@pytest.mark.parametrize("slice_", ["0", "1", "2"])
+@pytest.mark.parametrize("slice_", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("variant", range(8))
 def test_encode_crc64_every_flavour(engine, oracle, gpu, monkeypatch, variant, slice_):
     """All eight crc64.h flavours through the fused kernel, field-table,
-    slicing and hybrid paths (the u-domain paths byte-swap the norm flavours'
-    chains; the hybrid tables exist for load group 10, i.e. the k = 10 case)."""
+    slicing, hybrid and pipelined-slicing paths (the u-domain paths byte-swap
+    the norm flavours' chains; the hybrid and pipelined paths exist for load
+    group 10, i.e. the k = 10 case)."""
     _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", slice_)
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 10, 4, 4096 * 37 + 2048, 3, 0, 4,
                                 variant)
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 7, 3, 4096 * 20, 2, 0, 3, variant)
+
+
+@pytest.mark.parametrize("xrows", ["1", "0"])
+@pytest.mark.parametrize("nv", ["1", "2"])
+@pytest.mark.parametrize("k,rows,n,tt,variant", [
+    (10, 1, 4096 * 9, None, 0), (10, 2, 4096 * 11 + 1024, 3, 1), (10, 3, 4096 * 8, 2, 2),
+    (10, 4, 4096 * 37 + 2048, 4, 5), (20, 3, 4096 * 6 + 512, None, 7), (20, 4, 4096 * 5, 1, 3)])
+def test_encode_crc64_pipelined_rows(engine, oracle, gpu, monkeypatch, xrows, nv, k, rows, n, tt, variant):
+    """ISAL_HIP_CRC64_SLICE=3 (chain steps pipelined into the GF rows): every
+    row count it serves (1..4, rows split over its three stages, one or none
+    of them empty), one and two load groups of 10, row 0 derived or computed,
+    one and two lane groups == oracle."""
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", "3")
+    _setenv(monkeypatch, "ISAL_HIP_CRC_XROWS", xrows)
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_NV", nv)
+    test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, 3, 0, tt, variant)
 
 
 def test_encode_crc64_c2_full_size(engine, oracle, gpu):

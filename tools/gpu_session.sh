@@ -59,6 +59,18 @@ for s in $STEPS; do
                         ISAL_HIP_CRC64_SLICE=$sl run rocprof_encrc64_sl$sl 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_encrc64_sl$sl" -o e -- python3 bench.py --workload encode-crc64 --no-cpu-baseline
                 done
                 ;;
+        pipe64)
+                # fused encode+CRC64: byte tables (SL 1) vs chain steps pipelined into the GF rows (SL 3)
+                run pytest_gpu_pipe64 600 python -u -m pytest tests -m gpu -x -v -k "crc64_pipelined or encode_crc64_every_flavour or encode_crc64_slice_knobs" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for cfg in ${PIPE64_CFGS:-1:0 3:1 3:2}; do
+                                ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run bench_encrc64_sl${cfg/:/_nv}_r$r 300 python bench.py --workload encode-crc64 --no-cpu-baseline
+                        done
+                done
+                for cfg in ${PIPE64_PMC:-1:0 3:1}; do
+                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run pmc_lds_sl${cfg/:/_nv} 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_sl${cfg/:/_nv}" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
+                done
+                ;;
         fuzzgpu)
                 # differential fuzzing of the shipped library on the kernels (tests/fuzz)
                 python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null

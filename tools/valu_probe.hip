@@ -26,10 +26,16 @@
 constexpr int kIters = 2048;
 constexpr int kAcc = 8;  // independent chains per lane
 
-enum Op { ADD, PERM, BITOP3, XOR, SDWA_SHL, AND, BFE, LSHR, DS64_256, DS64_32, NOPS };
+enum Op { ADD, PERM, BITOP3, XOR, SDWA_SHL, AND, BFE, LSHR, DS64_256, DS64_32, PERM_S, BITOP3_S,
+          LDS_LIN, LDS_R256, LDS_R32, NOPS };
 static const char* kName[NOPS] = {"v_add_u32",   "v_perm_b32", "v_bitop3_b32", "v_xor_b32",
                                   "v_lshlrev_b32_sdwa", "v_and_b32", "v_bfe_u32", "v_lshrrev_b32",
-                                  "ds_read_b64 (256 x 8 B, random)", "ds_read_b64 (32 x 8 B, random)"};
+                                  "ds_read_b64 (256 x 8 B, random)", "ds_read_b64 (32 x 8 B, random)",
+                                  "v_perm_b32 (table in an SGPR, as the GF kernels)",
+                                  "v_bitop3_b32 (one SGPR operand)",
+                                  "ds_read_b64 throughput, lane-linear (conflict-free)",
+                                  "ds_read_b64 throughput, random entry of 256 x 8 B",
+                                  "ds_read_b64 throughput, random entry of 32 x 8 B"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void probe(uint32_t* out, uint32_t seed) {
@@ -40,6 +46,17 @@ __global__ __launch_bounds__(256) void probe(uint32_t* out, uint32_t seed) {
 #pragma unroll
   for (int i = 0; i < kAcc; ++i) a[i] = seed * (threadIdx.x + 17 * i + 1);
   const uint32_t b = seed ^ threadIdx.x, c = seed + 0x01020304u * threadIdx.x;
+  // LDS byte offsets of the throughput modes (fixed per lane: the same bank
+  // pattern every iteration): lane-linear, or random entries of a 2 KiB / 256 B table
+  uint32_t o[kAcc];
+#pragma unroll
+  for (int q = 0; q < kAcc; ++q) {
+    uint32_t h = (threadIdx.x * 8 + q + 1) * 0x9E3779B1u;
+    h ^= h >> 15;
+    h *= 0x85EBCA77u;
+    h ^= h >> 13;
+    o[q] = OP == LDS_LIN ? ((threadIdx.x & 31) * 8 + q * 256) % 2048 : OP == LDS_R256 ? (h & 0x7F8u) : (h & 0xF8u);
+  }
   for (int it = 0; it < kIters; ++it) {
 #pragma unroll
     for (int i = 0; i < kAcc; ++i) {
@@ -60,7 +77,23 @@ __global__ __launch_bounds__(256) void probe(uint32_t* out, uint32_t seed) {
         asm volatile("v_bfe_u32 %0, %0, 3, 8" : "+v"(a[i]));
       else if constexpr (OP == LSHR)
         asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a[i]));
-      else {
+      else if constexpr (OP == PERM_S)
+        asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(a[i]) : "s"(seed), "v"(c));
+      else if constexpr (OP == BITOP3_S)
+        asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[i]) : "s"(seed), "v"(c));
+      else if constexpr (OP == LDS_LIN || OP == LDS_R256 || OP == LDS_R32) {
+        if (i == 0) {  // 8 independent reads in flight per wave, then one wait
+          // volatile: re-read every iteration (the offsets do not change)
+          typedef const volatile __attribute__((address_space(3))) char lchar;
+          typedef const volatile __attribute__((address_space(3))) uint64_t lu64;
+          lchar* lv = (lchar*)(lt);
+          uint64_t v[kAcc];
+#pragma unroll
+          for (int q = 0; q < kAcc; ++q) v[q] = *(lu64*)(lv + o[q]);
+#pragma unroll
+          for (int q = 0; q < kAcc; ++q) a[q] ^= static_cast<uint32_t>(v[q]);
+        }
+      } else {
         // dependent chain through LDS: next offset from the loaded entry
         constexpr uint32_t mask = OP == DS64_256 ? 0x7F8u : 0xF8u;
         const uint64_t v = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(lt) + (a[i] & mask));
@@ -114,6 +147,11 @@ int main(int argc, char** argv) {
   ns[LSHR] = run<LSHR>(d, blocks, e0, e1);
   ns[DS64_256] = run<DS64_256>(d, blocks, e0, e1);
   ns[DS64_32] = run<DS64_32>(d, blocks, e0, e1);
+  ns[PERM_S] = run<PERM_S>(d, blocks, e0, e1);
+  ns[BITOP3_S] = run<BITOP3_S>(d, blocks, e0, e1);
+  ns[LDS_LIN] = run<LDS_LIN>(d, blocks, e0, e1);
+  ns[LDS_R256] = run<LDS_R256>(d, blocks, e0, e1);
+  ns[LDS_R32] = run<LDS_R32>(d, blocks, e0, e1);
   const double winstr = static_cast<double>(blocks) * 4 * kIters * kAcc;  // per op kind
   for (int o = 0; o < NOPS; ++o)
     printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"cus\": %d, \"ns\": %.0f, "
