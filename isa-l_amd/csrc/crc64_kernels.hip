@@ -608,43 +608,6 @@ __device__ __forceinline__ X64 fold8(const Look8& r) {
   return a;
 }
 
-// acc[l] ^= c[l][a] * x ^ c[l][b] * y for rows [L0, L1) (selectors and
-// coefficient tables already in registers).
-template <int P, int L0, int L1>
-__device__ __forceinline__ void mac_rows2(uint32_t (&acc)[P][4], const Sel (&sx)[4], const Sel (&sy)[4],
-                                          const Coef (&ca)[P], const Coef (&cb)[P]) {
-#pragma unroll
-  for (int l = L0; l < L1; ++l) {
-    const Coef& a = ca[l];
-    const Coef& b = cb[l];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t v = acc[l][d];
-      v = xor3(v, __builtin_amdgcn_perm(a.a1, a.a0, sx[d].s0), __builtin_amdgcn_perm(a.b1, a.b0, sx[d].s1));
-      v = xor3(v, __builtin_amdgcn_perm(0u, a.c, sx[d].s2), __builtin_amdgcn_perm(b.a1, b.a0, sy[d].s0));
-      v = xor3(v, __builtin_amdgcn_perm(b.b1, b.b0, sy[d].s1), __builtin_amdgcn_perm(0u, b.c, sy[d].s2));
-      acc[l][d] = v;
-    }
-  }
-}
-
-// The coefficient tables come in by scalar loads, which share lgkmcnt with
-// the LDS lookups and may complete out of order: a wait for one of them is a
-// wait for every lookup in flight. So a pair's tables are loaded and waited
-// for in its first stage, behind the fold that waits anyway.
-template <int P, int L0>
-__device__ __forceinline__ void load_coefs(Coef (&c)[P], const uint32_t* __restrict__ t) {
-#pragma unroll
-  for (int l = L0; l < P; ++l) c[l] = load_coef(t + l * kTbl);
-}
-
-template <int P, int L0>
-__device__ __forceinline__ void have_coefs(const Coef (&c)[P]) {
-#pragma unroll
-  for (int l = L0; l < P; ++l)
-    asm volatile("" ::"s"(c[l].a0), "s"(c[l].a1), "s"(c[l].b0), "s"(c[l].b1), "s"(c[l].c));
-}
-
 // One source pair; `car` holds the previous pair's second chain, its last
 // eight lookups in flight (cp = where its state goes; nullptr: none).
 template <int P, bool R0, int PH>

@@ -180,6 +180,45 @@ __device__ __forceinline__ void mac16x2(uint32_t (&acc)[P][4], const uint4& x, c
   }
 }
 
+// acc[l] ^= c[l][a] * x ^ c[l][b] * y for rows [L0, L1) (selectors and
+// coefficient tables already in registers; the fused kernels' pipelined
+// paths cut a source pair's rows into stages around their CRC lookups).
+template <int P, int L0, int L1>
+__device__ __forceinline__ void mac_rows2(uint32_t (&acc)[P][4], const Sel (&sx)[4], const Sel (&sy)[4],
+                                          const Coef (&ca)[P], const Coef (&cb)[P]) {
+#pragma unroll
+  for (int l = L0; l < L1; ++l) {
+    const Coef& a = ca[l];
+    const Coef& b = cb[l];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t v = acc[l][d];
+      v = xor3(v, __builtin_amdgcn_perm(a.a1, a.a0, sx[d].s0), __builtin_amdgcn_perm(a.b1, a.b0, sx[d].s1));
+      v = xor3(v, __builtin_amdgcn_perm(0u, a.c, sx[d].s2), __builtin_amdgcn_perm(b.a1, b.a0, sy[d].s0));
+      v = xor3(v, __builtin_amdgcn_perm(b.b1, b.b0, sy[d].s1), __builtin_amdgcn_perm(0u, b.c, sy[d].s2));
+      acc[l][d] = v;
+    }
+  }
+}
+
+// The coefficient tables come in by scalar loads, which share lgkmcnt with
+// LDS accesses and may complete out of order: a wait for one of them is a
+// wait for every LDS lookup in flight. The pipelined paths load a pair's
+// tables and wait for them (have_coefs) in its first stage, behind the fold
+// that waits anyway.
+template <int P, int L0, int L1 = P>
+__device__ __forceinline__ void load_coefs(Coef (&c)[P], const uint32_t* __restrict__ t) {
+#pragma unroll
+  for (int l = L0; l < L1; ++l) c[l] = load_coef(t + l * kTbl);
+}
+
+template <int P, int L0, int L1 = P>
+__device__ __forceinline__ void have_coefs(const Coef (&c)[P]) {
+#pragma unroll
+  for (int l = L0; l < L1; ++l)
+    asm volatile("" ::"s"(c[l].a0), "s"(c[l].a1), "s"(c[l].b0), "s"(c[l].b1), "s"(c[l].c));
+}
+
 // U sources j..j+U-1: issue all U loads before any arithmetic, then fold the
 // sources in pairs; the scheduling barriers keep one pair's temporaries live
 // at a time (otherwise the scheduler hoists every lookup and spills).

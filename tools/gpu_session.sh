@@ -71,6 +71,16 @@ for s in $STEPS; do
                         ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run pmc_lds_sl${cfg/:/_nv} 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_sl${cfg/:/_nv}" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
                 done
                 ;;
+        pipe32)
+                # fused encode+CRC32C: byte tables (NB 4) vs chain steps pipelined into the GF rows (NB 8)
+                run pytest_gpu_pipe32 600 python -u -m pytest tests -m gpu -x -v -k "crc_pipelined or encode_crc_byte_tables or crc64_pipelined" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for cfg in ${PIPE32_CFGS:-4:0 8:1 8:2}; do
+                                ISAL_HIP_CRC_BYTE_DWORDS=${cfg%:*} ISAL_HIP_CRC_FUSED_NV=${cfg#*:} run bench_encrc_nb${cfg/:/_nv}_r$r 300 python bench.py --workload encode-crc --no-cpu-baseline
+                        done
+                        run bench_encrc64_r$r 300 python bench.py --workload encode-crc64 --no-cpu-baseline
+                done
+                ;;
         fuzzgpu)
                 # differential fuzzing of the shipped library on the kernels (tests/fuzz)
                 python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
