@@ -364,7 +364,8 @@ bool shards_pre() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC_PRE) != 0;
 }
 
-// Full tiles loaded per batch (ISAL_HIP_CRC64_BATCH = 4 or 8).
+// Full tiles loaded per batch (ISAL_HIP_CRC64_BATCH = 4 or 8), in the
+// chain-step kernels and in the pre-shifted kernel's double buffer.
 int load_batch() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC64_BATCH) == 8 ? 8 : 4;
 }
@@ -1041,12 +1042,14 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
                      len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),      \
                      static_cast<unsigned>(g.nfull), d_tabs, part)
       const int m = chain_step(), b8 = load_batch() == 8;
-      if (vec16 && shards_pre())
-        hipLaunchKernelGGL(crc64_shards_pre<4>, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride,
-                           nsh, len, nitems, static_cast<unsigned>(g.nblk),
-                           static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull), !refl,
-                           d_tabs, part);
-      else if (!vec16)
+      if (vec16 && shards_pre()) {
+#define PRE_LAUNCH(B)                                                                                  \
+  hipLaunchKernelGGL(crc64_shards_pre<B>, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, \
+                     nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),             \
+                     static_cast<unsigned>(g.nfull), !refl, d_tabs, part)
+        if (b8) PRE_LAUNCH(8); else PRE_LAUNCH(4);
+#undef PRE_LAUNCH
+      } else if (!vec16)
         SHARDS_LAUNCH(false, 1, 4);
       else if (m == 4)
         { if (b8) SHARDS_LAUNCH(true, 4, 8); else SHARDS_LAUNCH(true, 4, 4); }

@@ -1026,6 +1026,17 @@ def test_crc64_c2_full_size(engine, oracle, gpu):
     b.close()
 
 
+@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("k,rows,n,ns,skew,tt", [CRC64_SHAPES[0], CRC64_SHAPES[1], CRC64_SHAPES[6],
+                                                 (3, 1, 4096 * 11 + 16, 2, 0, 7), (2, 1, 4096 * 19, 2, 0, 17)])
+def test_crc64_pre_batch8(engine, oracle, gpu, monkeypatch, variant, k, rows, n, ns, skew, tt):
+    """The pre-shifted checksum-only CRC64 kernel with 8 tiles per load batch
+    (ISAL_HIP_CRC64_BATCH=8: crc64_shards_pre<8>), incl. blocks shorter than a
+    batch and not a multiple of it, == oracle."""
+    _setenv(monkeypatch, "ISAL_HIP_CRC64_BATCH", "8")
+    test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, k, rows, n, ns, skew, tt)
+
+
 @pytest.mark.parametrize("batch", [4, 8])
 @pytest.mark.parametrize("step", [1, 2, 4])
 @pytest.mark.parametrize("k,rows,n,ns,skew,tt", [CRC64_SHAPES[0], CRC64_SHAPES[1], CRC64_SHAPES[6],

@@ -81,6 +81,14 @@ for s in $STEPS; do
                         run bench_encrc64_r$r 300 python bench.py --workload encode-crc64 --no-cpu-baseline
                 done
                 ;;
+        pre8)
+                # checksum-only CRC64: pre-shifted kernel with 4 or 8 tiles per load batch
+                for r in 1 2; do
+                        for b in 4 8; do
+                                ISAL_HIP_CRC64_BATCH=$b run bench_crc64_b${b}_r$r 300 python bench.py --workload crc64 --no-cpu-baseline
+                        done
+                done
+                ;;
         fuzzgpu)
                 # differential fuzzing of the shipped library on the kernels (tests/fuzz)
                 python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
