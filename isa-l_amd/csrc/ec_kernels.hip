@@ -231,11 +231,23 @@ int enc_group(int k) {
   return 4;
 }
 
+// Work order of the vector encode (ISAL_HIP_ENC_ORDER): 0 = (stripe, tile)
+// with tile fastest; 2 = XCD-contiguous (block b, dispatched round-robin to
+// XCD b % 8, takes item (b % 8) * nitems/8 + b / 8, so each XCD walks one
+// contiguous eighth of the stripes). Same items, same arithmetic.
+int enc_order() {
+  return isal_hip_knob(ISAL_HIP_KNOB_ENC_ORDER) == 2 ? 2 : 0;
+}
+
 template <int P, int U>
 void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
                 int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles) {
-  hipLaunchKernelGGL((ec_encode_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), 0, s, ptrs,
-                     ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
+  if (enc_order() == 2)
+    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>>), dim3(grid), dim3(kBlock), 0, s,
+                       ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
+  else
+    hipLaunchKernelGGL((ec_encode_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), 0, s, ptrs,
+                       ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
 }
 
 template <int P>

@@ -51,6 +51,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_PINNED_DIRECT] = {"ISAL_HIP_PINNED_DIRECT", NULL},
         [ISAL_HIP_KNOB_CPU_MAX_BYTES_PINNED] = {"ISAL_HIP_CPU_MAX_BYTES_PINNED", NULL},
         [ISAL_HIP_KNOB_PAR_COPY] = {"ISAL_HIP_PAR_COPY", NULL},
+        [ISAL_HIP_KNOB_ENC_ORDER] = {"ISAL_HIP_ENC_ORDER", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];

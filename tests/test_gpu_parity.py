@@ -328,6 +328,28 @@ def test_batch_encode_update_vs_oracle(engine, oracle, gpu):
     b.close()
 
 
+@pytest.mark.parametrize("k,rows,n,ns", [(10, 4, 65536 + 48, 37), (10, 4, 1 << 20, 16), (7, 3, 4096 * 3, 5)])
+def test_batch_encode_xcd_order_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns):
+    """The XCD-contiguous work order (ISAL_HIP_ENC_ORDER=2) covers every
+    (stripe, tile) exactly once: item counts divisible by 8 and not (the
+    identity order then), ragged tiles, == oracle on every stripe."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_ENC_ORDER", "2")
+    a = engine.gf_gen_rs_matrix(k + rows, k)
+    tbls = engine.ec_init_tables(k, rows, a[k * k:])
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 77)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.encode(0)
+    torch.cuda.synchronize()
+    h_data, h_cod = _host(data), _host(coding)
+    want = _oracle_encode_all(oracle, a[k * k:], k, rows, [[h_data[s, j] for j in range(k)] for s in range(ns)])
+    for s in range(ns):
+        for l in range(rows):
+            assert np.array_equal(h_cod[s, l], want[s][l]), (s, l)
+    b.close()
+
+
 def test_config_c1_cauchy_k4_p2_64k(engine, gpu):
     case = golden()["encode"][0]
     assert (case["k"], case["rows"], case["len"], case["gen"]) == (4, 2, 65536, "cauchy")

@@ -89,6 +89,16 @@ for s in $STEPS; do
                         done
                 done
                 ;;
+        order)
+                # encode work order: tile-fastest (0) vs XCD-contiguous (2), interleaved
+                run pytest_gpu_order 300 python -u -m pytest tests -m gpu -x -v -k "xcd_order" --timeout 200 --timeout-method thread
+                for r in 1 2 3; do
+                        for o in 0 2; do
+                                ISAL_HIP_ENC_ORDER=$o run bench_c2_order${o}_r$r 300 python bench.py --no-cpu-baseline
+                        done
+                done
+                rocm-smi --showbus > "$OUT/bus.txt" 2>&1 || true
+                ;;
         fuzzgpu)
                 # differential fuzzing of the shipped library on the kernels (tests/fuzz)
                 python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
