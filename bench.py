@@ -233,6 +233,12 @@ def timed_steps(d: Dist, step, sync, steps: int, warmup: int):
     return d.max(t1 - t0)
 
 
+def enc_order() -> int:
+    """Work order the engine's vector encode launches with (ec_kernels.hip:enc_order):
+    2 = XCD-contiguous (default), 0 = tile-fastest (ISAL_HIP_ENC_ORDER=0)."""
+    return 0 if os.environ.get("ISAL_HIP_ENC_ORDER") == "0" else 2
+
+
 def enc_group(k: int) -> int:
     """Sources per load group the engine launches with (ec_kernels.hip:enc_group)."""
     return next((u for u in (12, 10, 8, 6, 5, 4) if k >= u and k % u == 0), 4)
@@ -600,7 +606,7 @@ def total_stripes_run(args, d: Dist, a, k, p, n):
         "self_check": bad == 0 and encoded == T * args.steps,
         "roofline": {
             "bound": "hbm",
-            "kernel": f"ec_encode_v16<{p}, EncPol<{enc_group(k)}, 2, 2, 0>>",
+            "kernel": f"ec_encode_v16<{p}, EncPol<{enc_group(k)}, 2, 2, {enc_order()}>>",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -756,7 +762,7 @@ def main(argv=None):
                                [int(frag(s, i).data_ptr()) for s in range(S) for i in surv],
                                [int(out[s, i].data_ptr()) for s in range(S) for i in range(rows)])
         bytes_per_launch = (k + rows) * n * S
-        kernel = f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, 2, 2, 0>>"
+        kernel = f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, 2, 2, {enc_order()}>>"
         workload = f"C3 decode: recover data shards {errs} of k={k} p={p} RS, {n} B shards x {S} stripes/GPU"
     else:
         rows = p
@@ -765,7 +771,7 @@ def main(argv=None):
                                [int(out[s, l].data_ptr()) for s in range(S) for l in range(p)])
         if args.workload == "encode":
             bytes_per_launch = (k + p) * n * S
-            kernel = f"ec_encode_v16<{p}, EncPol<{enc_group(k)}, 2, 2, 0>>"
+            kernel = f"ec_encode_v16<{p}, EncPol<{enc_group(k)}, 2, 2, {enc_order()}>>"
             workload = f"C2 encode: k={k} p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU"
         elif args.workload in ("encode-crc", "crc"):
             # fragment checksums: crc32_iscsi of all k+p shards,

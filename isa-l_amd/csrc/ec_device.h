@@ -94,7 +94,10 @@ __device__ __forceinline__ void store16(uint64_t base, long long off, uint4 v, i
 // Measured on MI355X (profiles/r01_probe_variants_*.txt): non-temporal loads
 // AND stores lift the 10-read/4-write stream from 5.5 to 6.1 TB/s, issuing
 // all of a stripe's source loads at once (U = k) adds ~1 %, buffer ops ~1 %;
-// the work order and shard padding do not help. The library picks U from k
+// shard padding does not help. The XCD-contiguous order (2) measured -2.4 %
+// on one round-1/2 box and +1.0-1.3 % on every round-3 box (same-box A/B,
+// profiles/r03_enc_order_benches.jsonl, r03_probe_variants.txt); the library
+// launches order 2 by default (ec_kernels.hip enc_order) and picks U from k
 // at launch (enc_group).
 template <int UU, int LDM = kBufNT, int STM = kBufNT, int ORD = 0>
 struct EncPol {

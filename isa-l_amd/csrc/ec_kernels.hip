@@ -231,12 +231,15 @@ int enc_group(int k) {
   return 4;
 }
 
-// Work order of the vector encode (ISAL_HIP_ENC_ORDER): 0 = (stripe, tile)
-// with tile fastest; 2 = XCD-contiguous (block b, dispatched round-robin to
-// XCD b % 8, takes item (b % 8) * nitems/8 + b / 8, so each XCD walks one
-// contiguous eighth of the stripes). Same items, same arithmetic.
+// Work order of the vector encode (ISAL_HIP_ENC_ORDER): 2 (default) =
+// XCD-contiguous (block b, dispatched round-robin to XCD b % 8, takes item
+// (b % 8) * nitems/8 + b / 8, so each XCD walks one contiguous eighth of the
+// stripes; the identity order when nitems % 8 != 0); 0 = (stripe, tile) with
+// tile fastest. Same items, same arithmetic. C2, same box, three runs each:
+// 2.401 -> 2.379 ms and 2.464 -> 2.436 ms on two boxes
+// (profiles/r03_enc_order_benches.jsonl; the memory probe: +1.2 %).
 int enc_order() {
-  return isal_hip_knob(ISAL_HIP_KNOB_ENC_ORDER) == 2 ? 2 : 0;
+  return isal_hip_knob(ISAL_HIP_KNOB_ENC_ORDER) == 0 ? 0 : 2;
 }
 
 template <int P, int U>
