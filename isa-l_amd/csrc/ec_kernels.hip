@@ -42,13 +42,22 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U>())) void ec_encode_v1
     if constexpr (Pol::ORDER == 0) {
       stripe = w / tiles;
       tile = w - stripe * tiles;
-    } else if constexpr (Pol::ORDER == 2) {
+    } else if constexpr (Pol::ORDER == 2 || Pol::ORDER == 3 || Pol::ORDER == 5) {
       // XCD-contiguous: blocks b, b+8, b+16.. (one XCD under round-robin
-      // dispatch) walk one contiguous eighth of the items. Speed only.
-      const unsigned per = nitems >> 3;
-      const unsigned v = (nitems & 7) ? w : (w & 7) * per + (w >> 3);
+      // dispatch) walk one contiguous eighth of the items (order 2); orders
+      // 3 and 5 (probes) cut the items into 16 / 32 ranges instead, two / four
+      // per XCD. Speed only.
+      constexpr unsigned G = Pol::ORDER == 2 ? 8 : Pol::ORDER == 3 ? 16 : 32;
+      const unsigned per = nitems / G;
+      const unsigned v = (nitems % G) ? w : (w % G) * per + w / G;
       stripe = v / tiles;
       tile = v - stripe * tiles;
+    } else if constexpr (Pol::ORDER == 4) {
+      // probe: XCD x streams whole stripes s = x (mod 8), tile fastest
+      const unsigned j = w >> 3, x = w & 7;
+      const unsigned sj = j / tiles;
+      stripe = (nstripes & 7) ? w / tiles : sj * 8 + x;
+      tile = (nstripes & 7) ? w - (w / tiles) * tiles : j - sj * tiles;
     } else {
       tile = w / nstripes;
       stripe = w - tile * nstripes;

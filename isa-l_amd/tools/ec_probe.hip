@@ -314,6 +314,9 @@ int main(int argc, char** argv) {
   using PBUF10 = EncPol<10, kBufNT, kBufNT, 0>;
   using PBUF10X = EncPol<10, kBufNT, kBufNT, 2>;
   using PBUF5 = EncPol<5, kBufNT, kBufNT, 0>;
+  using PBUF10G16 = EncPol<10, kBufNT, kBufNT, 3>;
+  using PBUF10G32 = EncPol<10, kBufNT, kBufNT, 5>;
+  using PBUF10SX = EncPol<10, kBufNT, kBufNT, 4>;
   ENC(EncDefault, 0, "encode default (buf U4)")
   ENC(PNB, 0, "encode U4 nt-both")
   ENC(PNB10, 0, "encode U10 nt-both")
@@ -321,6 +324,9 @@ int main(int argc, char** argv) {
   ENC(PBUF10, 0, "encode U10 buf-nt")
   ENC(PBUF10X, 0, "encode U10 buf-nt xcd-contig")
   ENC(PBUF5, 0, "encode U5 buf-nt")
+  ENC(PBUF10G16, 0, "encode U10 buf-nt 16 ranges")
+  ENC(PBUF10G32, 0, "encode U10 buf-nt 32 ranges")
+  ENC(PBUF10SX, 0, "encode U10 buf-nt stripes mod 8 per XCD")
 #define ENCP(POL, Q, NAME)                                                                     \
   V.push_back({NAME, enc_bytes, [=](hipStream_t st) {                                          \
                  hipLaunchKernelGGL((ec_encode_v16<4, POL>), dim3(nitems), dim3(256), 0, st,     \
