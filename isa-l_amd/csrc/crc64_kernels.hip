@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
                                                            unsigned nitems, unsigned nblk,
                                                            unsigned tt, unsigned nfull, int uswap,
                                                            const uint64_t* __restrict__ tabs,
-                                                           uint64_t* __restrict__ part) {
+                                                           uint64_t* __restrict__ part, int xcd) {
   __shared__ uint64_t lt[2 * kCE];  // F_u, F'_u
   load_lds<2 * kCE>(lt, tabs + ISAL_HIP_CRC64_PRE_TAB);
   __syncthreads();
@@ -247,7 +247,8 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
       chunk_acc(c, lt + kCE, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
     return c;
   };
-  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+  for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
+    const unsigned w = xcd_item(ww, nitems, xcd);
     const unsigned si = w / nblk, blk = w - si * nblk;
     const unsigned stripe = si / nsh, i = si - stripe * nsh;
     const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
@@ -698,7 +699,7 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
     const uint64_t* __restrict__ ptrs, int ptr_stride, const uint32_t* __restrict__ tbl, int len,
     int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged, int pair,
     unsigned long long x0src, int uswap, const uint64_t* __restrict__ tabs,
-    uint64_t* __restrict__ part) {
+    uint64_t* __restrict__ part, int xcd) {
   __shared__ uint64_t lt[SL == 2 ? kHyLds : SL ? kSlLds : kKernTab + kCE + kOp];
   extern __shared__ uint64_t la[];  // [k][kBlock * NV] source chains when !REG
   if constexpr (SL == 2) {
@@ -725,7 +726,8 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
   };
   const int nsh = k + P;
   const long long lane = tid * kVec;
-  for (unsigned w = blockIdx.x * NV + threadIdx.x / kBlock; w < nitems; w += gridDim.x * NV) {
+  for (unsigned ww = blockIdx.x * NV + threadIdx.x / kBlock; ww < nitems; ww += gridDim.x * NV) {
+    const unsigned w = xcd_item(ww, nitems, xcd, NV);
     const unsigned stripe = w / nblk, blk = w - stripe * nblk;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const unsigned t0 = blk * tt, t1 = t0 + tt < nfull ? t0 + tt : nfull;
@@ -928,7 +930,8 @@ void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_
   hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, REG, X0, SL, NV>), dim3((grid + NV - 1) / NV),     \
                      dim3(kBlock * NV), REG ? 0 : lds * NV, s, ptrs, ptr_stride, tbl, len, k,      \
                      nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),          \
-                     static_cast<unsigned>(g.nfull), ragged, pair_step(), xr.src[0], !refl, tabs, part)
+                     static_cast<unsigned>(g.nfull), ragged, pair_step(), xr.src[0], !refl, tabs, part, \
+                     xcd_order())
 #define FUSED64_X0(REG, SL, NV)                                                                    \
   do {                                                                                             \
     if (xr.rows & 1u) FUSED64_LAUNCH(REG, true, SL, NV); else FUSED64_LAUNCH(REG, false, SL, NV); \
@@ -1046,7 +1049,7 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
 #define PRE_LAUNCH(B)                                                                                  \
   hipLaunchKernelGGL(crc64_shards_pre<B>, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, \
                      nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),             \
-                     static_cast<unsigned>(g.nfull), !refl, d_tabs, part)
+                     static_cast<unsigned>(g.nfull), !refl, d_tabs, part, xcd_order())
         if (b8) PRE_LAUNCH(8); else PRE_LAUNCH(4);
 #undef PRE_LAUNCH
       } else if (!vec16)

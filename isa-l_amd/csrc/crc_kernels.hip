@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards_pre(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int idx0, int nsh, int len,
     unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, unsigned ntiles,
     const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part, uint32_t* __restrict__ tail,
-    int nshard_total, int shard0) {
+    int nshard_total, int shard0, int xcd) {
   __shared__ uint32_t lt[kPreFZ + ISAL_HIP_CRC_CHUNK_DWORDS];
   for (int i = threadIdx.x; i < kPreFZ; i += kBlock) lt[i] = tabs[i];
   for (int i = threadIdx.x; i < ISAL_HIP_CRC_CHUNK_DWORDS; i += kBlock)
@@ -296,7 +296,8 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards_pre(
     return t + 1 == tf ? chunk_map(lt + kPreF, x.x ^ b, x.y, x.z, x.w)
                        : chunk_map(lt + kPreFZ, x.x ^ b, x.y, x.z, x.w);
   };
-  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+  for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
+    const unsigned w = xcd_item(ww, nitems, xcd);
     const unsigned si = w / nblk, blk = w - si * nblk;
     const unsigned stripe = si / nsh, i = si - stripe * nsh;
     const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + idx0 + i];
@@ -540,7 +541,7 @@ __global__ __launch_bounds__(kBlock * NV, (crc_waves<P, Pol::U, REG>())) void ec
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned nblk, unsigned tt,
     unsigned nfull, unsigned ntiles, unsigned long long x0src, const uint32_t* __restrict__ tabs,
-    uint32_t* __restrict__ part, uint32_t* __restrict__ tail, int nshard_total, int out_shard0) {
+    uint32_t* __restrict__ part, uint32_t* __restrict__ tail, int nshard_total, int out_shard0, int xcd) {
   static_assert(!X0 || SRC, "row 0 is derived from this pass's source chains");
   static_assert(NB == 0 || NB == 4, "byte path: all four dwords");
   constexpr int kFull = SRC ? (REG ? kFeedReg : kFeedLds) : kFeedNone;
@@ -577,7 +578,8 @@ __global__ __launch_bounds__(kBlock * NV, (crc_waves<P, Pol::U, REG>())) void ec
     else
       body(std::integral_constant<bool, false>{});
   };
-  for (unsigned w = blockIdx.x * NV + threadIdx.x / kBlock; w < nitems; w += gridDim.x * NV) {
+  for (unsigned ww = blockIdx.x * NV + threadIdx.x / kBlock; ww < nitems; ww += gridDim.x * NV) {
+    const unsigned w = xcd_item(ww, nitems, xcd, NV);
     const unsigned stripe = w / nblk, blk = w - stripe * nblk;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const size_t shard_s = static_cast<size_t>(stripe) * nshard_total;  // source shard 0
@@ -750,7 +752,7 @@ void launch_fused(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs
                      src0, dst0, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),               \
                      static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull),                  \
                      static_cast<unsigned>(g.ntiles), xr.src[0], tabs, part, tail, nshard_total,   \
-                     out_shard0)
+                     out_shard0, xcd_order())
   const bool x0 = crc_src && (xr.rows & 1u);
   const bool nb4 = crc_byte_dwords() == 4;
   const bool nv2 = nb4 && crc_src && fused_nv32(k) == 2;
@@ -843,7 +845,8 @@ extern "C" int isal_hip_launch_crc(const uint64_t* d_ptrs, int ptr_stride, int i
       hipLaunchKernelGGL(crc32c_shards_pre, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
                          ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
                          static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
-                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
+                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0,
+                         xcd_order());
     else if (!vec16)
       CRC_SHARDS(false, 1);
     else if (crc_step() == 4)

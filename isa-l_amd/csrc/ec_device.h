@@ -109,6 +109,22 @@ template <int UU>
 using EncNT = EncPol<UU>;
 using EncDefault = EncNT<4>;
 
+// Item of work index w in the XCD-contiguous order: workgroup u runs on XCD
+// u % 8 (round-robin dispatch), and with the order on its nv items come from
+// the (u % 8)-th contiguous eighth of [0, n), so each XCD streams one region
+// (the encode's order 2). A bijection of [0, n); the identity when
+// off or when n is not a multiple of 8 * nv.
+__device__ __forceinline__ unsigned xcd_item(unsigned w, unsigned n, int on, unsigned nv = 1) {
+  if (!on || n % (8 * nv)) return w;
+  const unsigned u = w / nv, g = w - u * nv, per = n / (8 * nv);
+  return ((u & 7) * per + (u >> 3)) * nv + g;
+}
+
+// ISAL_HIP_XCD_ORDER: the update and CRC kernels' item order (host side).
+[[maybe_unused]] int xcd_order() {
+  return isal_hip_knob(ISAL_HIP_KNOB_XCD_ORDER) == 1;
+}
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU op (gfx950)
 }

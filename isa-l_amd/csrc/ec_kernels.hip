@@ -175,8 +175,9 @@ template <int P>
 __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restrict__ ptrs,
                                                         int ptr_stride, int src_idx, int dst0,
                                                         const uint32_t* __restrict__ tbl, int len,
-                                                        unsigned nitems, unsigned tiles) {
-  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+                                                        unsigned nitems, unsigned tiles, int xcd) {
+  for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
+    const unsigned w = xcd_item(ww, nitems, xcd);
     const unsigned stripe = w / tiles;
     const unsigned tile = w - stripe * tiles;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
@@ -294,7 +295,7 @@ hipError_t update_pass(const uint64_t* ptrs, int ptr_stride, int src_idx, int ds
   const unsigned nitems = nstripes * tiles;
   if (vec16)
     hipLaunchKernelGGL(ec_update_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
-                       ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
+                       ptr_stride, src_idx, dst0, tbl, len, nitems, tiles, xcd_order());
   else
     hipLaunchKernelGGL(ec_update_b1<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);

@@ -350,6 +350,40 @@ def test_batch_encode_xcd_order_vs_oracle(engine, oracle, gpu, monkeypatch, k, r
     b.close()
 
 
+def test_xcd_item_order_update_and_checksums(engine, oracle, gpu, monkeypatch):
+    """ISAL_HIP_XCD_ORDER=1 (update, checksum-only and fused CRC kernels take
+    their items XCD-contiguously): item counts that are multiples of 8 (the
+    remapped order) and not (the identity), one and two lane groups, == oracle."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_XCD_ORDER", "1")
+    # update: 16 stripes x 17 tiles (a multiple of 8 items) and 37 x 16 + 48 bytes
+    for k, rows, n, ns in [(10, 4, 4096 * 17, 16), (10, 4, 65536 + 48, 37)]:
+        a = engine.gf_gen_rs_matrix(k + rows, k)
+        tbls = engine.ec_init_tables(k, rows, a[k * k:])
+        data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 91)
+        b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+        for v in range(k):
+            b.update(v, 0)
+        torch.cuda.synchronize()
+        h_data, h_cod = _host(data), _host(coding)
+        want = _oracle_encode_all(oracle, a[k * k:], k, rows, [[h_data[s, j] for j in range(k)] for s in range(ns)])
+        for s in range(ns):
+            for l in range(rows):
+                assert np.array_equal(h_cod[s, l], want[s][l]), (k, n, s, l)
+        b.close()
+    for nv in ("1", "2"):
+        _setenv(monkeypatch, "ISAL_HIP_CRC_FUSED_NV", nv)
+        _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_NV", nv)
+        test_encode_crc_vs_oracle(engine, oracle, gpu, 10, 4, 4096 * 64 * 2, 8, 0)
+        test_encode_crc_vs_oracle(engine, oracle, gpu, 10, 4, 4096 * 37 + 2048, 5, 0)
+        test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 10, 4, 4096 * 64 * 2, 8, 0, None, 1)
+        test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 10, 4, 4096 * 37 + 2048, 3, 0, 4, 5)
+    for variant in (0, 5):
+        test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, 10, 4, 4096 * 64 * 2, 8, 0, None)
+        test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, 5, 2, 4096 * 40, 2, 0, 16)
+
+
 def test_config_c1_cauchy_k4_p2_64k(engine, gpu):
     case = golden()["encode"][0]
     assert (case["k"], case["rows"], case["len"], case["gen"]) == (4, 2, 65536, "cauchy")

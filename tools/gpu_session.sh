@@ -99,6 +99,18 @@ for s in $STEPS; do
                 done
                 rocm-smi --showbus > "$OUT/bus.txt" 2>&1 || true
                 ;;
+        xcd)
+                # update / CRC kernels: tile-fastest items vs XCD-contiguous items (ISAL_HIP_XCD_ORDER)
+                run pytest_gpu_xcd 300 python -u -m pytest tests -m gpu -x -v -k "xcd" --timeout 200 --timeout-method thread
+                for r in 1 2; do
+                        for o in 0 1; do
+                                for wl in "update --k 20 --p 6 --len 4194304 --stripes 64" "crc" "crc64" "encode-crc" "encode-crc64"; do
+                                        tag=$(echo $wl | cut -d' ' -f1)
+                                        ISAL_HIP_XCD_ORDER=$o run bench_${tag}_x${o}_r$r 300 python bench.py --workload $wl --no-cpu-baseline
+                                done
+                        done
+                done
+                ;;
         fuzzgpu)
                 # differential fuzzing of the shipped library on the kernels (tests/fuzz)
                 python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
