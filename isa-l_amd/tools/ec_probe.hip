@@ -324,6 +324,10 @@ int main(int argc, char** argv) {
   ENC(PBUF10, 0, "encode U10 buf-nt")
   ENC(PBUF10X, 0, "encode U10 buf-nt xcd-contig")
   ENC(PBUF5, 0, "encode U5 buf-nt")
+  ENC(PBUF10X, 2048, "encode U10 buf-nt xcd-contig grid 2048")
+  ENC(PBUF10X, 4096, "encode U10 buf-nt xcd-contig grid 4096")
+  ENC(PBUF10X, 16384, "encode U10 buf-nt xcd-contig grid 16384")
+  ENC(PBUF10, 4096, "encode U10 buf-nt grid 4096")
   ENC(PBUF10G16, 0, "encode U10 buf-nt 16 ranges")
   ENC(PBUF10G32, 0, "encode U10 buf-nt 32 ranges")
   ENC(PBUF10SX, 0, "encode U10 buf-nt stripes mod 8 per XCD")
