@@ -798,7 +798,9 @@ def main(argv=None):
                             f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
             else:
                 batch.encode(torch.cuda.current_stream(dev).cuda_stream)
-                kernel = "crc32c_shards<true>"
+                # pre-shifted chains by default, chain-step kernel under ISAL_HIP_CRC_PRE=0
+                kernel = ("crc32c_shards<true>" if os.environ.get("ISAL_HIP_CRC_PRE") == "0"
+                          else "crc32c_shards_pre")
                 workload = (f"CRC32C (crc32_iscsi) of all k+p={k + p} shards, {n} B x {S} "
                             f"stripes/GPU, device-resident")
         elif args.workload == "encode-crc64":
@@ -833,7 +835,13 @@ def main(argv=None):
             crc_out = torch.zeros(S * (k + p), dtype=torch.int64, device=dev)
             bytes_per_launch = (k + p) * n * S
             batch.encode(torch.cuda.current_stream(dev).cuda_stream)
-            kernel = "crc64_shards<true, 2, 4>"
+            b8 = 8 if os.environ.get("ISAL_HIP_CRC64_BATCH") == "8" else 4
+            if os.environ.get("ISAL_HIP_CRC_PRE") == "0":
+                m = {"1": 1, "4": 4}.get(os.environ.get("ISAL_HIP_CRC64_STEP", ""), 2)
+                kernel = f"crc64_shards<true, {m}, {b8}>"
+            else:
+                pp = str(os.environ.get("ISAL_HIP_CRC64_PRE_PIPE") == "1").lower()
+                kernel = f"crc64_shards_pre<{b8}, {pp}>"
             workload = (f"CRC64 (crc64_ecma_refl) of all k+p={k + p} shards, {n} B x {S} "
                         f"stripes/GPU, device-resident")
         else:

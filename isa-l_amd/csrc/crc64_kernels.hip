@@ -228,7 +228,43 @@ __global__ __launch_bounds__(kBlock) void crc64_shards(const uint64_t* __restric
 // maps the chunk once, b' = F'_u(chunk ^ b) — 28 lookups per tile and no chain
 // step (M = 2 spends 35) — the item's last tile applies F_u and leaves the
 // plain chain. Loads are double-buffered (the next B tiles in flight).
-template <int B>
+//
+// PIPE (ISAL_HIP_CRC64_PRE_PIPE=1, a measured negative result, see pre_pipe()):
+// the compiler emits chunk_acc as pairs of ds_read_b64 with an
+// s_waitcnt after every pair, so a tile is 14 dependent LDS round trips. Only
+// the first 8 bytes' 14 lookups depend on the chain; the last 8 bytes' do not.
+// The pipelined form issues a tile's 14 chain-dependent lookups, folds the
+// independent 14 issued one tile earlier, issues the next tile's independent
+// 14, then folds the dependent ones: one LDS round trip per tile on the chain.
+// Volatile LDS loads + scheduling barriers keep the issue order (as in the
+// fused kernel's SL 3 stages). Same tables and arithmetic.
+struct Look14 {
+  uint64_t v[14];
+};
+
+__device__ __forceinline__ uint64_t tab_issue(const uint64_t* t, int f, uint32_t o) {
+  typedef const __attribute__((address_space(3))) char lchar;
+  typedef const volatile __attribute__((address_space(3))) uint64_t lu64;
+  return *(lu64*)((lchar*)(t) + f * 256 + o);
+}
+
+// Issue the 14 field lookups of (w0, w1) in the 14 tables at t.
+__device__ __forceinline__ void issue14(Look14& r, const uint64_t* t, uint32_t w0, uint32_t w1) {
+  uint32_t o[kF], q[kF];
+  field_offsets8(w0, o);
+  field_offsets8(w1, q);
+#pragma unroll
+  for (int f = 0; f < kF; ++f) r.v[f] = tab_issue(t, f, o[f]);
+#pragma unroll
+  for (int f = 0; f < kF; ++f) r.v[kF + f] = tab_issue(t, kF + f, q[f]);
+}
+
+__device__ __forceinline__ void fold14(X64& acc, const Look14& r) {
+#pragma unroll
+  for (int i = 0; i < 14; i += 2) acc.add2(r.v[i], r.v[i + 1]);
+}
+
+template <int B, bool PIPE = true>
 __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __restrict__ ptrs,
                                                            int ptr_stride, int nsh, int len,
                                                            unsigned nitems, unsigned nblk,
@@ -239,6 +275,7 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
   load_lds<2 * kCE>(lt, tabs + ISAL_HIP_CRC64_PRE_TAB);
   __syncthreads();
   const long long lane = threadIdx.x * kVec;
+  constexpr int D2 = 2 * kF * 32;  // tables of the chunk's last 8 bytes
   auto step = [&](unsigned t, unsigned t1, X64 b, const uint4& x) __attribute__((always_inline)) {
     X64 c{0u, 0u};
     if (t + 1 == t1)
@@ -246,6 +283,26 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
     else
       chunk_acc(c, lt + kCE, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
     return c;
+  };
+  // B tiles with the lookups pipelined (PIPE). LAST: the batch ends the item,
+  // so its last tile uses F_u (a compile-time table base keeps every lookup's
+  // table offset in the ds_read immediate).
+  auto batch = [&](auto last_c, X64 b, const uint4 (&x)[B]) __attribute__((always_inline)) {
+    constexpr bool LAST = decltype(last_c)::value;
+    Look14 ind, dep;
+    issue14(ind, (LAST && B == 1 ? lt : lt + kCE) + D2, x[0].z, x[0].w);
+#pragma unroll
+    for (int g = 0; g < B; ++g) {
+      issue14(dep, LAST && g + 1 == B ? lt : lt + kCE, x[g].x ^ b.lo, x[g].y ^ b.hi);
+      __builtin_amdgcn_sched_barrier(0);
+      X64 c{0u, 0u};
+      fold14(c, ind);
+      if (g + 1 < B) issue14(ind, (LAST && g + 2 == B ? lt : lt + kCE) + D2, x[g + 1].z, x[g + 1].w);
+      __builtin_amdgcn_sched_barrier(0);
+      fold14(c, dep);
+      b = c;
+    }
+    return b;
   };
   for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
     const unsigned w = xcd_item(ww, nitems, xcd);
@@ -269,8 +326,15 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
         for (int g = 0; g < B; ++g)
           xn[g] = load16<kBufNT>(base, static_cast<long long>(t + B + g) * kTile + lane, len);
       }
+      if constexpr (PIPE) {
+        if (t + B == t1)
+          b = batch(std::true_type{}, b, x);
+        else
+          b = batch(std::false_type{}, b, x);
+      } else {
 #pragma unroll
-      for (int g = 0; g < B; ++g) b = step(t + g, t1, b, x[g]);
+        for (int g = 0; g < B; ++g) b = step(t + g, t1, b, x[g]);
+      }
     }
     for (; t < t1; ++t)
       b = step(t, t1, b, load16<kBufNT>(base, static_cast<long long>(t) * kTile + lane, len));
@@ -363,6 +427,16 @@ int chain_step() {
 // chain-step kernels above, with ISAL_HIP_CRC64_STEP / _BATCH).
 bool shards_pre() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC_PRE) != 0;
+}
+
+// Pipelined lookups in the pre-shifted kernel (ISAL_HIP_CRC64_PRE_PIPE=1; off
+// by default). C2 shape, same box, two runs each
+// (profiles/r03_crc64_prepipe_benches.jsonl, r03_pmc_sq_crc64_prepipe.txt):
+// 2.82-2.85 ms unpipelined vs 2.94-2.95 ms pipelined — SQ_WAIT_INST_LDS fell
+// 41 % but the 56 lookup VGPRs in flight cut the occupancy from 7 to 3 waves
+// per SIMD, and the kernel was not bound by its LDS round trips.
+bool pre_pipe() {
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_PRE_PIPE) == 1;
 }
 
 // Full tiles loaded per batch (ISAL_HIP_CRC64_BATCH = 4 or 8), in the
@@ -1046,11 +1120,12 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
                      static_cast<unsigned>(g.nfull), d_tabs, part)
       const int m = chain_step(), b8 = load_batch() == 8;
       if (vec16 && shards_pre()) {
-#define PRE_LAUNCH(B)                                                                                  \
-  hipLaunchKernelGGL(crc64_shards_pre<B>, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, \
-                     nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),             \
+#define PRE_LAUNCH(B, PP)                                                                               \
+  hipLaunchKernelGGL((crc64_shards_pre<B, PP>), dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, \
+                     len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),          \
                      static_cast<unsigned>(g.nfull), !refl, d_tabs, part, xcd_order())
-        if (b8) PRE_LAUNCH(8); else PRE_LAUNCH(4);
+        if (pre_pipe()) { if (b8) PRE_LAUNCH(8, true); else PRE_LAUNCH(4, true); }
+        else { if (b8) PRE_LAUNCH(8, false); else PRE_LAUNCH(4, false); }
 #undef PRE_LAUNCH
       } else if (!vec16)
         SHARDS_LAUNCH(false, 1, 4);

@@ -81,6 +81,21 @@ for s in $STEPS; do
                         run bench_encrc64_r$r 300 python bench.py --workload encode-crc64 --no-cpu-baseline
                 done
                 ;;
+        prepipe)
+                # checksum-only CRC64: pre-shifted kernel with pipelined lookups (1, default) vs not (0)
+                run pytest_gpu_crc64 400 python -u -m pytest tests -m gpu -x -v -k "crc64 and not encode" --timeout 200 --timeout-method thread
+                for r in 1 2; do
+                        for pp in 0 1; do
+                                for b in ${PP_BATCHES:-4}; do
+                                        ISAL_HIP_CRC64_PRE_PIPE=$pp ISAL_HIP_CRC64_BATCH=$b run bench_crc64_pp${pp}_b${b}_r$r 300 python bench.py --workload crc64 --no-cpu-baseline
+                                done
+                        done
+                done
+                for pp in 0 1; do
+                        ISAL_HIP_CRC64_PRE_PIPE=$pp run pmc_lds_crc64_pp$pp 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_crc64_pp$pp" -o l -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 2 --warmup 1
+                done
+                run rocprof_crc64 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_crc64" -o crc64 -- python3 bench.py --workload crc64 --no-cpu-baseline
+                ;;
         pre8)
                 # checksum-only CRC64: pre-shifted kernel with 4 or 8 tiles per load batch
                 for r in 1 2; do
