@@ -50,15 +50,19 @@ typedef u32x4 __attribute__((address_space(1)))* gstore_t;
 // 2 non-temporal buffer_load/store (wave-uniform descriptor per shard, 32-bit
 // lane offset; measured +1.3 % over mode 1 on the 10-read/4-write stream,
 // profiles/r01_probe_variants_3.txt). `len` bounds the buffer descriptor.
-enum : int { kPlain = 0, kNT = 1, kBufNT = 2 };
+// 3 = buffer ops with sc1 + nt (gfx950 CPol 0x12): in the memory probe the
+// 10-read/4-write stream with sc1+nt stores ran +0.5-0.9 % over nt stores
+// (profiles/r03_probe_variants.txt); selectable for the encode's stores.
+enum : int { kPlain = 0, kNT = 1, kBufNT = 2, kBufSC1NT = 3 };
 
 template <int MODE = kPlain>
 __device__ __forceinline__ uint4 load16(uint64_t base, long long off, int len = 0) {
   u32x4 v;
-  if constexpr (MODE == kBufNT) {
+  if constexpr (MODE == kBufNT || MODE == kBufSC1NT) {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
-    const v4i r = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(off), 0, 2 /* nt */);
+    const v4i r = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(off), 0,
+                                                        MODE == kBufNT ? 2 /* nt */ : 0x12 /* sc1 nt */);
     v = {static_cast<uint32_t>(r.x), static_cast<uint32_t>(r.y), static_cast<uint32_t>(r.z),
          static_cast<uint32_t>(r.w)};
   } else if constexpr (MODE == kNT) {
@@ -71,12 +75,13 @@ __device__ __forceinline__ uint4 load16(uint64_t base, long long off, int len = 
 
 template <int MODE = kPlain>
 __device__ __forceinline__ void store16(uint64_t base, long long off, uint4 v, int len = 0) {
-  if constexpr (MODE == kBufNT) {
+  if constexpr (MODE == kBufNT || MODE == kBufSC1NT) {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
     const v4i w = {static_cast<int>(v.x), static_cast<int>(v.y), static_cast<int>(v.z),
                    static_cast<int>(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(w, rs, static_cast<int>(off), 0, 2 /* nt */);
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, static_cast<int>(off), 0,
+                                           MODE == kBufNT ? 2 /* nt */ : 0x12 /* sc1 nt */);
   } else {
     u32x4 w = {v.x, v.y, v.z, v.w};
     if constexpr (MODE == kNT)

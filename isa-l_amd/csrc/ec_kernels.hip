@@ -252,10 +252,19 @@ int enc_order() {
   return isal_hip_knob(ISAL_HIP_KNOB_ENC_ORDER) == 0 ? 0 : 2;
 }
 
+// Store policy of the vector encode (ISAL_HIP_ENC_STORE=1: sc1 + nt buffer
+// stores, an A/B knob; default nt).
+bool enc_store_sc1() {
+  return isal_hip_knob(ISAL_HIP_KNOB_ENC_STORE) == 1;
+}
+
 template <int P, int U>
 void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
                 int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles) {
-  if (enc_order() == 2)
+  if (enc_order() == 2 && enc_store_sc1())
+    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufSC1NT, 2>>), dim3(grid), dim3(kBlock), 0, s,
+                       ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
+  else if (enc_order() == 2)
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>>), dim3(grid), dim3(kBlock), 0, s,
                        ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
   else

@@ -118,6 +118,7 @@ enum {
         ISAL_HIP_KNOB_PAR_COPY,        /* 0: one thread issues a staged call's copies (no helper) */
         ISAL_HIP_KNOB_ENC_ORDER,       /* encode work order: 2 XCD-contiguous (default), 0 tile-fastest */
         ISAL_HIP_KNOB_XCD_ORDER,       /* update / CRC kernels: 1 XCD-contiguous items */
+        ISAL_HIP_KNOB_ENC_STORE,       /* vector encode stores: 1 sc1 + nt (A/B) | nt */
         ISAL_HIP_KNOB_CRC64_PRE_PIPE,  /* checksum-only CRC64: 1 pipelined lookups (slower; off) */
         ISAL_HIP_KNOB_COUNT
 };

@@ -53,6 +53,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_PAR_COPY] = {"ISAL_HIP_PAR_COPY", NULL},
         [ISAL_HIP_KNOB_ENC_ORDER] = {"ISAL_HIP_ENC_ORDER", NULL},
         [ISAL_HIP_KNOB_XCD_ORDER] = {"ISAL_HIP_XCD_ORDER", NULL},
+        [ISAL_HIP_KNOB_ENC_STORE] = {"ISAL_HIP_ENC_STORE", NULL},
         [ISAL_HIP_KNOB_CRC64_PRE_PIPE] = {"ISAL_HIP_CRC64_PRE_PIPE", NULL},
 };
 

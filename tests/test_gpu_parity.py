@@ -328,14 +328,17 @@ def test_batch_encode_update_vs_oracle(engine, oracle, gpu):
     b.close()
 
 
+@pytest.mark.parametrize("store", ["0", "1"])
 @pytest.mark.parametrize("k,rows,n,ns", [(10, 4, 65536 + 48, 37), (10, 4, 1 << 20, 16), (7, 3, 4096 * 3, 5)])
-def test_batch_encode_xcd_order_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns):
+def test_batch_encode_xcd_order_vs_oracle(engine, oracle, gpu, monkeypatch, store, k, rows, n, ns):
     """The XCD-contiguous work order (ISAL_HIP_ENC_ORDER=2) covers every
     (stripe, tile) exactly once: item counts divisible by 8 and not (the
-    identity order then), ragged tiles, == oracle on every stripe."""
+    identity order then), ragged tiles, == oracle on every stripe; with nt
+    and with sc1 + nt parity stores (ISAL_HIP_ENC_STORE=1)."""
     import torch
 
     _setenv(monkeypatch, "ISAL_HIP_ENC_ORDER", "2")
+    _setenv(monkeypatch, "ISAL_HIP_ENC_STORE", store)
     a = engine.gf_gen_rs_matrix(k + rows, k)
     tbls = engine.ec_init_tables(k, rows, a[k * k:])
     data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 77)

@@ -136,6 +136,22 @@ for s in $STEPS; do
                 # the driver's N>1 form on this one-GPU box: two gloo ranks share the GPU
                 run bench_gpus2_gloo 300 python bench.py --gpus 2 --dist-backend gloo --no-cpu-baseline
                 ;;
+        encstore)
+                # encode parity stores: nt (0, default) vs sc1 + nt (1), interleaved
+                run pytest_gpu_encstore 300 python -u -m pytest tests -m gpu -x -v -k "xcd_order_vs_oracle" --timeout 200 --timeout-method thread
+                for r in 1 2 3; do
+                        for st in 0 1; do
+                                ISAL_HIP_ENC_STORE=$st run bench_c2_store${st}_r$r 300 python bench.py --no-cpu-baseline
+                        done
+                done
+                ;;
+        gpus8)
+                # rehearsal of the driver's N=8 launch forms on this one-GPU box: eight gloo
+                # ranks share the GPU (RCCL needs one GPU per rank), 128 stripes per rank
+                run bench_gpus8_gloo 300 python bench.py --gpus 8 --dist-backend gloo --stripes 128 --no-cpu-baseline
+                run bench_gpus4_torchrun_gloo 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 4 --dist-backend gloo --stripes 128 --no-cpu-baseline
+                run bench_c5_gpus8_gloo 300 python bench.py --gpus 8 --dist-backend gloo --total-stripes 8192 --stripes 128 --steps 2 --warmup 1 --no-cpu-baseline
+                ;;
         tests_crc)
                 run pytest_gpu_crc 300 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
                 ;;
