@@ -266,10 +266,11 @@ def pmc_traffic(workload, k, p, n, S, kernel):
     import statistics
 
     want = {"workload": workload, "k": str(k), "p": str(p), "len": str(n), "stripes": str(S)}
-    def norm(x):
-        return x.replace("(anonymous namespace)::", "").replace(" ", "")
+    def norm(x):  # rocprof prints "void " before template kernels only
+        x = x.replace("(anonymous namespace)::", "").replace(" ", "")
+        return x[4:] if x.startswith("void") else x
 
-    name = "void" + norm(kernel)
+    name = norm(kernel)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_*.csv")), reverse=True):
         with open(path) as f:
             lines = f.read().splitlines()
