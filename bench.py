@@ -800,7 +800,8 @@ def main(argv=None):
             else:
                 batch.encode(torch.cuda.current_stream(dev).cuda_stream)
                 # pre-shifted chains by default, chain-step kernel under ISAL_HIP_CRC_PRE=0
-                kernel = ("crc32c_shards<true>" if os.environ.get("ISAL_HIP_CRC_PRE") == "0"
+                m32 = 4 if os.environ.get("ISAL_HIP_CRC_STEP") == "4" else 1
+                kernel = (f"crc32c_shards<true, {m32}>" if os.environ.get("ISAL_HIP_CRC_PRE") == "0"
                           else "crc32c_shards_pre")
                 workload = (f"CRC32C (crc32_iscsi) of all k+p={k + p} shards, {n} B x {S} "
                             f"stripes/GPU, device-resident")
