@@ -1,0 +1,220 @@
+/*
+ * dropin_bench.c — throughput of the synchronous drop-in ec_encode_data on
+ * device-resident shards (the way the reference's API is driven: one call
+ * per stripe, erasure_code/erasure_code_perf.c:126-132), from T threads.
+ *
+ * usage: dropin_bench K P LEN STRIPES THREADS SECONDS [CALLS_PER_THREAD]
+ *
+ * STRIPES stripes of K + P shards live in HBM (one hipMalloc, shard s*(K+P)+i
+ * at offset ((s*(K+P)+i) * LEN)); thread t encodes stripes t, t+T, ... in a
+ * loop, one ec_encode_data(LEN, K, P, gftbls, data, coding) per stripe, for
+ * SECONDS (or exactly CALLS_PER_THREAD calls each when given, for traces).
+ * Prints one JSON object: calls, wall seconds, us per call (one thread's view:
+ * wall / calls per thread), calls/s and GiB/s of (K+P)*LEN per call (the
+ * reference's perf_print convention, erasure_code_perf.c:304).
+ *
+ * Self-check (no oracle): for the first and last stripe, 8192 sampled columns
+ * of every parity row are recomputed on the host from the library's host GF
+ * math (gf_mul of the generator matrix, itself pinned by the reference's
+ * golden fixtures) and compared.
+ *
+ * Build: make -C isa-l_amd tools  (gcc, links libisal_hip.so + libamdhip64).
+ */
+#include <hip/hip_runtime_api.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "erasure_code.h"
+
+static double
+now(void)
+{
+        struct timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        return (double) t.tv_sec + (double) t.tv_nsec * 1e-9;
+}
+
+typedef struct {
+        int t, nthreads, k, p, len, stripes;
+        long long fixed_calls;
+        unsigned char *base, *tbls;
+        double deadline;
+        long long calls;
+        double first_call_us;
+} worker_t;
+
+static unsigned char *
+shard(const worker_t *w, int s, int i)
+{
+        return w->base + ((size_t) s * (size_t) (w->k + w->p) + (size_t) i) * (size_t) w->len;
+}
+
+static void *
+run(void *arg)
+{
+        worker_t *w = (worker_t *) arg;
+        unsigned char *data[256], *coding[256];
+        int s = w->t, i;
+        (void) hipSetDevice(0);
+        w->calls = 0;
+        for (;;) {
+                double t0;
+                if (w->fixed_calls ? w->calls >= w->fixed_calls : now() >= w->deadline)
+                        break;
+                for (i = 0; i < w->k; i++)
+                        data[i] = shard(w, s, i);
+                for (i = 0; i < w->p; i++)
+                        coding[i] = shard(w, s, w->k + i);
+                t0 = w->calls ? 0 : now();
+                ec_encode_data(w->len, w->k, w->p, w->tbls, data, coding);
+                if (!w->calls)
+                        w->first_call_us = (now() - t0) * 1e6;
+                w->calls++;
+                s += w->nthreads;
+                if (s >= w->stripes)
+                        s = w->t % w->stripes;
+        }
+        return NULL;
+}
+
+/* parity columns of stripe s recomputed on the host from gf_mul and the
+ * generator rows; 0 on match */
+static int
+check_stripe(const worker_t *w, const unsigned char *a, int s)
+{
+        const int k = w->k, p = w->p, len = w->len, ncol = len < 8192 ? len : 8192;
+        unsigned char *src = malloc((size_t) k * len), *par = malloc((size_t) p * len);
+        int i, l, c, bad = 0;
+        uint64_t x = 88172645463325252ull + (uint64_t) s;
+        if (!src || !par)
+                return 1;
+        for (i = 0; i < k; i++)
+                (void) hipMemcpy(src + (size_t) i * len, shard(w, s, i), (size_t) len, hipMemcpyDeviceToHost);
+        for (l = 0; l < p; l++)
+                (void) hipMemcpy(par + (size_t) l * len, shard(w, s, k + l), (size_t) len, hipMemcpyDeviceToHost);
+        for (c = 0; c < ncol && !bad; c++) {
+                int col;
+                x ^= x << 13;
+                x ^= x >> 7;
+                x ^= x << 17;
+                col = c < 64 ? c : c >= ncol - 64 ? len - (ncol - c) : (int) (x % (uint64_t) len);
+                for (l = 0; l < p; l++) {
+                        unsigned char acc = 0;
+                        for (i = 0; i < k; i++)
+                                acc ^= gf_mul(a[(k + l) * k + i], src[(size_t) i * len + col]);
+                        if (acc != par[(size_t) l * len + col]) {
+                                fprintf(stderr, "dropin_bench: stripe %d row %d col %d: got %u want %u\n", s, l,
+                                        col, par[(size_t) l * len + col], acc);
+                                bad = 1;
+                        }
+                }
+        }
+        free(src);
+        free(par);
+        return bad;
+}
+
+int
+main(int argc, char **argv)
+{
+        int k, p, len, stripes, nthreads, i, ok;
+        double seconds, t0, wall;
+        long long calls = 0, fixed = 0;
+        size_t total, nsrc_bytes;
+        unsigned char *a, *tbls, *base, *h;
+        uint64_t x = 0x9E3779B97F4A7C15ull;
+        worker_t *w;
+        pthread_t *th;
+        hipError_t e;
+
+        if (argc < 7) {
+                fprintf(stderr, "usage: %s K P LEN STRIPES THREADS SECONDS [CALLS_PER_THREAD]\n", argv[0]);
+                return 2;
+        }
+        k = atoi(argv[1]);
+        p = atoi(argv[2]);
+        len = atoi(argv[3]);
+        stripes = atoi(argv[4]);
+        nthreads = atoi(argv[5]);
+        seconds = atof(argv[6]);
+        if (argc > 7)
+                fixed = atoll(argv[7]);
+        if (k < 1 || p < 1 || k + p > 255 || len < 1 || stripes < 1 || nthreads < 1 || nthreads > 256) {
+                fprintf(stderr, "dropin_bench: bad arguments\n");
+                return 2;
+        }
+        if (stripes < nthreads)
+                stripes = nthreads;
+        total = (size_t) stripes * (size_t) (k + p) * (size_t) len;
+        if ((e = hipMalloc((void **) &base, total)) != hipSuccess) {
+                fprintf(stderr, "dropin_bench: hipMalloc(%zu): %s\n", total, hipGetErrorString(e));
+                return 1;
+        }
+        /* sources random, parity zero; one host stripe of random bytes copied
+         * into every stripe with a per-stripe byte rotation */
+        nsrc_bytes = (size_t) k * (size_t) len;
+        h = malloc(nsrc_bytes);
+        if (!h)
+                return 1;
+        for (size_t b = 0; b < nsrc_bytes; b++) {
+                x ^= x << 13;
+                x ^= x >> 7;
+                x ^= x << 17;
+                h[b] = (unsigned char) (x >> 32);
+        }
+        (void) hipMemset(base, 0, total);
+        for (i = 0; i < stripes; i++) {
+                const size_t rot = ((size_t) i * 977) % nsrc_bytes;
+                unsigned char *dst = base + (size_t) i * (size_t) (k + p) * (size_t) len;
+                (void) hipMemcpy(dst, h + rot, nsrc_bytes - rot, hipMemcpyHostToDevice);
+                if (rot)
+                        (void) hipMemcpy(dst + nsrc_bytes - rot, h, rot, hipMemcpyHostToDevice);
+        }
+        free(h);
+        (void) hipDeviceSynchronize();
+
+        a = malloc((size_t) (k + p) * (size_t) k);
+        tbls = malloc((size_t) 32 * (size_t) k * (size_t) p);
+        w = calloc((size_t) nthreads, sizeof(*w));
+        th = calloc((size_t) nthreads, sizeof(*th));
+        if (!a || !tbls || !w || !th)
+                return 1;
+        gf_gen_rs_matrix(a, k + p, k);
+        ec_init_tables(k, p, a + (size_t) k * k, tbls);
+
+        for (i = 0; i < nthreads; i++) {
+                w[i] = (worker_t){.t = i, .nthreads = nthreads, .k = k, .p = p, .len = len,
+                                  .stripes = stripes, .fixed_calls = fixed, .base = base, .tbls = tbls};
+        }
+        /* warm every thread's context (stream, argument buffers) first */
+        for (i = 0; i < nthreads; i++) {
+                w[i].fixed_calls = 2;
+                pthread_create(&th[i], NULL, run, &w[i]);
+        }
+        for (i = 0; i < nthreads; i++)
+                pthread_join(th[i], NULL);
+        t0 = now();
+        for (i = 0; i < nthreads; i++) {
+                w[i].fixed_calls = fixed;
+                w[i].deadline = t0 + seconds;
+                pthread_create(&th[i], NULL, run, &w[i]);
+        }
+        for (i = 0; i < nthreads; i++) {
+                pthread_join(th[i], NULL);
+                calls += w[i].calls;
+        }
+        wall = now() - t0;
+        ok = check_stripe(&w[0], a, 0) == 0 && check_stripe(&w[0], a, stripes - 1) == 0;
+        printf("{\"k\": %d, \"p\": %d, \"len\": %d, \"stripes\": %d, \"threads\": %d, \"calls\": %lld, "
+               "\"wall_s\": %.4f, \"us_per_call\": %.2f, \"calls_per_s\": %.1f, \"gib_s\": %.3f, "
+               "\"first_timed_call_us_thread0\": %.1f, \"self_check\": %s}\n",
+               k, p, len, stripes, nthreads, calls, wall, wall / ((double) calls / nthreads) * 1e6,
+               (double) calls / wall, (double) calls * (double) (k + p) * (double) len / wall / (double) (1 << 30),
+               w[0].first_call_us, ok ? "true" : "false");
+        (void) hipFree(base);
+        return ok ? 0 : 1;
+}

@@ -152,6 +152,39 @@ for s in $STEPS; do
                 run bench_gpus4_torchrun_gloo 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 4 --dist-backend gloo --stripes 128 --no-cpu-baseline
                 run bench_c5_gpus8_gloo 300 python bench.py --gpus 8 --dist-backend gloo --total-stripes 8192 --stripes 128 --steps 2 --warmup 1 --no-cpu-baseline
                 ;;
+        steady)
+                # C2 headline kernel: per-dispatch trace, steady-state average of the
+                # K timed launches (tools/kernel_stats.py), beside the bench line
+                run bench_c2 300 python bench.py --no-cpu-baseline
+                cp "$OUT/bench_c2.log" "$OUT/bench_c2.json"
+                run rocprof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c2" -o c2 -- python3 bench.py --no-cpu-baseline
+                run steady_c2 60 python3 tools/kernel_stats.py "$OUT/prof_c2" ec_encode_v16 --skip 5 --keep 20 --bytes 15032385536 --out "$OUT/c2_encode_kernel_steady.csv" --config "workload=encode k=10 p=4 len=1048576 stripes=1024" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline"
+                ;;
+        wide)
+                # wide-stripe encode: device-resident shapes beyond C2's p = 4
+                for shape in ${WIDE_SHAPES:-"20 6 4194304 64" "10 8 1048576 1024" "10 6 1048576 1024" "10 4 1048576 1024"}; do
+                        set -- ${shape//_/ }
+                        tag=k$1p$2
+                        args="--workload encode --k $1 --p $2 --len $3 --stripes $4 --no-cpu-baseline"
+                        bytes=$(( ($1 + $2) * $3 * $4 ))
+                        run bench_$tag 300 python bench.py $args
+                        cp "$OUT/bench_$tag.log" "$OUT/bench_$tag.json"
+                        run rocprof_$tag 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$tag" -o $tag -- python3 bench.py $args
+                        run steady_$tag 60 python3 tools/kernel_stats.py "$OUT/prof_$tag" ec_encode_v16 --skip 5 --keep 20 --bytes $bytes --out "$OUT/${tag}_encode_kernel_steady.csv" --config "workload=encode k=$1 p=$2 len=$3 stripes=$4" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py $args"
+                        run pmc_fetch_$tag 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$tag" -o f -- python3 bench.py $args --steps 3 --warmup 1
+                        run pmc_write_$tag 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$tag" -o w -- python3 bench.py $args --steps 3 --warmup 1
+                        python3 tools/pmc_csv.py "$OUT/pmc_$tag.csv" "workload=encode k=$1 p=$2 len=$3 stripes=$4" "python bench.py $args --steps 3 --warmup 1" "$OUT/pmc_fetch_$tag" "$OUT/pmc_write_$tag" ec_encode_v16
+                        run pmc_sq_$tag 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_$tag" -o s -- python3 bench.py $args --steps 2 --warmup 1
+                done
+                ;;
+        dropin)
+                # the synchronous drop-in call on device-resident C2 stripes, 1/4/16 threads
+                for t in 1 4 16; do
+                        run dropin_t$t 120 tools/dropin_bench 10 4 1048576 64 $t 3
+                done
+                run dropin_small_t1 120 tools/dropin_bench 10 4 4096 64 1 3
+                run dropin_hiptrace 200 rocprofv3 --hip-trace --kernel-trace --stats --output-format csv -d "$OUT/prof_dropin" -o dropin -- tools/dropin_bench 10 4 1048576 64 1 0 400
+                ;;
         tests_crc)
                 run pytest_gpu_crc 300 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
                 ;;
