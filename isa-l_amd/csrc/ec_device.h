@@ -243,28 +243,69 @@ __device__ __forceinline__ void have_coefs(const Coef (&c)[P]) {
     asm volatile("" ::"s"(c[l].a0), "s"(c[l].a1), "s"(c[l].b0), "s"(c[l].b1), "s"(c[l].c));
 }
 
+// Encode variants (template FL of chunk16 / accum16 / ec_encode_v16):
+//   kEncLUT  every product through the v_perm lookups;
+//   kEncXor  the pass's row 0 and its column of source 0 hold only 0/1
+//            (isal_hip_encmask; every gf_gen_rs_matrix and RAID P+Q block):
+//            row 0 is acc ^= x & m (one VALU op per dword instead of three
+//            v_perm, their folds and a table move), and source 0 starts every
+//            row's sum as x & m (no lookups, no XOR). Masks arrive as kernel
+//            arguments: r0m bit j for row 0's source j, c0m bit l for source
+//            0's row l.
+enum : int { kEncLUT = 0, kEncXor = 1 };
+
+// Source pairs share XOR3s but hold two sources' tables in SGPRs (5 dwords per
+// looked-up row each): pairs while at most 4 rows per source are looked up
+// (wider passes paired spilled SGPRs, even with the row tables loaded in
+// groups of two rows).
+template <int P, int FL>
+constexpr int enc_pair() {
+  return (P - (FL == kEncXor ? 1 : 0)) <= 4 ? 2 : 1;
+}
+
 // U sources j..j+U-1: issue all U loads before any arithmetic, then fold the
 // sources in pairs; the scheduling barriers keep one pair's temporaries live
 // at a time (otherwise the scheduler hoists every lookup and spills).
-template <int P, int U, int MODE = kPlain>
+// kEncXor: source j of the group is folded on its own — at j == 0 it starts
+// every row's sum as x & m (acc must be zero), in later groups it is an
+// ordinary lookup — and the pairs are (j+1, j+2), ...: one loop body for
+// both, so the register budget is that of one group.
+template <int P, int U, int MODE = kPlain, int FL = kEncLUT>
 __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
                                         int j, long long off, const uint32_t* __restrict__ tbl,
-                                        int len) {
+                                        int len, unsigned long long r0m = 0, unsigned c0m = 0) {
+  constexpr bool X = FL == kEncXor;
   uint4 x[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
-  // Pairs share XOR3s but hold two sources' tables (2*P*5 SGPRs): only for P <= 4.
-  constexpr int PAIR = P <= 4 ? 2 : 1;
+  constexpr int U0 = X ? 1 : 0;
+  if constexpr (X) {
+    if (j == 0) {
 #pragma unroll
-  for (int u = 0; u + PAIR <= U; u += PAIR) {
-    if constexpr (PAIR == 2)
-      mac16x2<P>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl);
-    else
-      mac16<P>(acc, x[u], tbl + (j + u) * P * kTbl);
+      for (int l = 0; l < P; ++l) {
+        const uint32_t m = (c0m >> l) & 1u ? ~0u : 0u;
+        acc[l][0] = x[0].x & m;
+        acc[l][1] = x[0].y & m;
+        acc[l][2] = x[0].z & m;
+        acc[l][3] = x[0].w & m;
+      }
+    } else {
+      mac16<P, true>(acc, x[0], tbl + j * P * kTbl, r0_mask(r0m, j));
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
-  if constexpr (PAIR == 2 && (U & 1)) {
-    mac16<P>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl);
+  constexpr int PAIR = enc_pair<P, FL>();
+#pragma unroll
+  for (int u = U0; u + PAIR <= U; u += PAIR) {
+    if constexpr (PAIR == 2)
+      mac16x2<P, X>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl,
+                    X ? r0_mask(r0m, j + u) : 0u, X ? r0_mask(r0m, j + u + 1) : 0u);
+    else
+      mac16<P, X>(acc, x[u], tbl + (j + u) * P * kTbl, X ? r0_mask(r0m, j + u) : 0u);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (PAIR == 2 && ((U - U0) & 1)) {
+    mac16<P, X>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl, X ? r0_mask(r0m, j + U - 1) : 0u);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -313,31 +354,36 @@ __device__ __forceinline__ void dot_bytes(const uint64_t* __restrict__ sp, int s
 // Waves per SIMD the register allocator must allow (VGPR budget 512/waves).
 // Live VGPRs ~ 4U (loads in flight) + 4P (accumulators) + ~32 (selectors,
 // table halves, addresses); the 512-entry file gives 512/alloc waves per SIMD.
-template <int P, int U>
+// The kEncXor variant (FL 1) keeps a source's raw dwords live beside its
+// selectors (row 0 is x & m): 8 more VGPRs; so do P >= 6 and the verify
+// kernel (FL 2, which also holds the stored parity): without them these
+// spilled to scratch (`make -C isa-l_amd isa` reports every kernel's budget).
+template <int P, int U, int FL = 0>
 constexpr int enc_waves() {
-  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8;
+  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8 + (FL == 1 ? 8 : 0) + (P >= 6 ? 8 : 0) +
+                      (FL == 2 ? 16 : 0);
   constexpr int w = 512 / est;
   return w > 8 ? 8 : (w < 4 ? 4 : w);
 }
 
 // acc[l] = XOR_j c[l][j] * src[j][off..off+16) for one lane.
-template <int P, class Pol>
+template <int P, class Pol, int FL = kEncLUT>
 __device__ __forceinline__ void accum16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
                                         const uint32_t* __restrict__ tbl, int k, long long off,
-                                        int len) {
+                                        int len, unsigned long long r0m = 0, unsigned c0m = 0) {
 #pragma unroll
   for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
   int j = 0;
-  for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::LD>(acc, src, j, off, tbl, len);
+  for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m);
   // Remainder. The launcher only picks U > 4 when U divides k, so there the
   // (cheap, correct for any k) single-source loop is dead in practice.
   if constexpr (Pol::U == 4) {
     if (j + 2 <= k) {
-      chunk16<P, 2, Pol::LD>(acc, src, j, off, tbl, len);
+      chunk16<P, 2, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m);
       j += 2;
     }
   }
-  for (; j < k; ++j) chunk16<P, 1, Pol::LD>(acc, src, j, off, tbl, len);
+  for (; j < k; ++j) chunk16<P, 1, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m);
 }
 
 }  // namespace

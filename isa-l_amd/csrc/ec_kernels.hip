@@ -32,10 +32,12 @@
 namespace {
 
 
-template <int P, class Pol = EncDefault>
-__global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U>())) void ec_encode_v16(
-    const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
-    const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles) {
+// The work items of an encode launch: (stripe, 4 KiB column tile) pairs.
+template <int P, class Pol, int FL>
+__device__ __forceinline__ void encode_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
+                                             int dst0, const uint32_t* __restrict__ tbl, int len, int k,
+                                             unsigned nitems, unsigned tiles, unsigned long long r0m,
+                                             unsigned c0m) {
   const unsigned nstripes = nitems / tiles;
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     unsigned stripe, tile;
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U>())) void ec_encode_v1
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
       uint32_t acc[P][4];
-      accum16<P, Pol>(acc, sp + src0, tbl, k, off, len);
+      accum16<P, Pol, FL>(acc, sp + src0, tbl, k, off, len, r0m, c0m);
 #pragma unroll
       for (int l = 0; l < P; ++l)
         store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
@@ -75,6 +77,28 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U>())) void ec_encode_v1
       dot_bytes<P>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off));
     }
   }
+}
+
+template <int P, class Pol = EncDefault, int FL = kEncLUT>
+__global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encode_v16(
+    const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
+    const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles,
+    unsigned long long r0m, unsigned c0m) {
+  encode_items<P, Pol, FL>(ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+}
+
+// One stripe whose shard pointers and coefficient tables travel as kernel
+// arguments (isal_hip_karg, 2 KiB): the synchronous drop-in call on
+// device-resident shards launches this with no argument upload before it
+// (a hipMemcpyAsync + blit kernel per call otherwise).
+template <int P, class Pol, int FL>
+__global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encode_karg(
+    const isal_hip_karg a, int len, int k, unsigned tiles, unsigned long long r0m, unsigned c0m) {
+  // `a` is the first argument, at offset 0 of the kernarg segment: read it in
+  // place (scalar loads) — indexing the by-value copy with runtime indices
+  // made the compiler copy all 2 KiB of it to scratch.
+  const auto* ka = reinterpret_cast<const isal_hip_karg*>(__builtin_amdgcn_kernarg_segment_ptr());
+  encode_items<P, Pol, FL>(ka->ptrs, k + P, 0, k, ka->tbl, len, k, tiles, tiles, r0m, c0m);
 }
 
 // Any alignment: one lane per byte column, 256 columns per work item.
@@ -98,7 +122,7 @@ __global__ __launch_bounds__(kBlock) void ec_encode_b1(const uint64_t* __restric
 // is reduced into *bad with atomicMin. Nothing is written to the shards.
 // ---------------------------------------------------------------------------
 template <int P>
-__global__ __launch_bounds__(kBlock, (enc_waves<P, 4>())) void ec_verify_v16(
+__global__ __launch_bounds__(kBlock, (enc_waves<P, 4, 2>())) void ec_verify_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles,
     unsigned long long* __restrict__ slots, int row0, long long col0) {
@@ -258,35 +282,43 @@ bool enc_store_sc1() {
   return isal_hip_knob(ISAL_HIP_KNOB_ENC_STORE) == 1;
 }
 
+// XOR fast path (isal_hip_encmask) only in the default policy: XCD-contiguous
+// order, nt buffer loads and stores.
 template <int P, int U>
 void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
-                int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles) {
+                int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles,
+                bool x, unsigned long long r0m, unsigned c0m) {
   if (enc_order() == 2 && enc_store_sc1())
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufSC1NT, 2>>), dim3(grid), dim3(kBlock), 0, s,
-                       ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
+                       ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
+  else if (enc_order() == 2 && x)
+    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncXor>), dim3(grid), dim3(kBlock), 0,
+                       s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
   else if (enc_order() == 2)
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>>), dim3(grid), dim3(kBlock), 0, s,
-                       ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
+                       ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
   else
     hipLaunchKernelGGL((ec_encode_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), 0, s, ptrs,
-                       ptr_stride, src0, dst0, tbl, len, k, nitems, tiles);
+                       ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
 }
 
 template <int P>
 hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0, const uint32_t* tbl,
-                       int len, int k, unsigned nstripes, bool vec16, hipStream_t s) {
+                       int len, int k, unsigned nstripes, bool vec16, bool x, unsigned long long r0m,
+                       unsigned c0m, hipStream_t s) {
   const unsigned span = vec16 ? kTile : kBlock;
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
   const unsigned nitems = nstripes * tiles;
   const unsigned grid = grid_for(nitems);
   if (vec16) {
     switch (enc_group(k)) {
-      case 12: launch_v16<P, 12>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
-      case 10: launch_v16<P, 10>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
-      case 8: launch_v16<P, 8>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
-      case 6: launch_v16<P, 6>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
-      case 5: launch_v16<P, 5>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
-      default: launch_v16<P, 4>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles); break;
+#define EC_GROUP(u)                                                                                   \
+  case u:                                                                                             \
+    launch_v16<P, u>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, x, r0m, c0m); \
+    break;
+      EC_GROUP(12) EC_GROUP(10) EC_GROUP(8) EC_GROUP(6) EC_GROUP(5)
+#undef EC_GROUP
+      default: launch_v16<P, 4>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, x, r0m, c0m); break;
     }
   } else {
     hipLaunchKernelGGL(ec_encode_b1<P>, dim3(grid), dim3(kBlock), 0, s, ptrs, ptr_stride, src0,
@@ -324,7 +356,8 @@ unsigned stripes_per_launch(int len, bool vec16) {
 
 extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, int src_idx0,
                                       int dst_idx0, const uint32_t* d_tbl, int len, int k, int rows,
-                                      long long nstripes, int vec16, void* stream) {
+                                      long long nstripes, int vec16, const isal_hip_encmask* em,
+                                      void* stream) {
   if (len <= 0 || rows <= 0 || nstripes <= 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned per = stripes_per_launch(len, vec16 != 0);
@@ -335,11 +368,15 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
       const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
       const uint32_t* tbl = d_tbl + static_cast<size_t>(kTbl) * k * r0;
       const int dst0 = dst_idx0 + r0;
+      const int g = r0 / EC_MAX_ROWS_PER_PASS;
+      const bool x = em && g < EC_MAX_PASSES && ((em->ok >> g) & 1u);
+      const unsigned long long r0m = x ? em->r0[g] : 0ull;
+      const unsigned c0m = x ? em->c0[g] : 0u;
       hipError_t e = hipSuccess;
       switch (P) {
-#define EC_CASE(n)                                                                            \
-  case n:                                                                                     \
-    e = encode_pass<n>(ptrs, ptr_stride, src_idx0, dst0, tbl, len, k, ns, vec16 != 0, s); \
+#define EC_CASE(n)                                                                                      \
+  case n:                                                                                               \
+    e = encode_pass<n>(ptrs, ptr_stride, src_idx0, dst0, tbl, len, k, ns, vec16 != 0, x, r0m, c0m, s); \
     break;
         EC_CASE(1) EC_CASE(2) EC_CASE(3) EC_CASE(4) EC_CASE(5) EC_CASE(6) EC_CASE(7) EC_CASE(8)
 #undef EC_CASE
@@ -348,6 +385,37 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
     }
   }
   return 0;
+}
+
+extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int k, int rows,
+                                           const isal_hip_encmask* em, void* stream) {
+  if (len <= 0 || rows <= 0) return 0;
+  if (rows > EC_MAX_ROWS_PER_PASS || k + rows > ISAL_HIP_KARG_PTRS ||
+      static_cast<size_t>(kTbl) * k * rows > ISAL_HIP_KARG_TBL)
+    return static_cast<int>(hipErrorInvalidValue);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + kTile - 1) / kTile);
+  const bool x = em && (em->ok & 1u);
+  const unsigned long long r0m = x ? em->r0[0] : 0ull;
+  const unsigned c0m = x ? em->c0[0] : 0u;
+  switch (rows * 16 + enc_group(k)) {
+#define EC_KARG(n, u)                                                                                   \
+  case n * 16 + u:                                                                                      \
+    if (x)                                                                                              \
+      hipLaunchKernelGGL((ec_encode_karg<n, EncPol<u, kBufNT, kBufNT, 2>, kEncXor>), dim3(tiles),         \
+                         dim3(kBlock), 0, s, *a, len, k, tiles, r0m, c0m);                              \
+    else                                                                                                \
+      hipLaunchKernelGGL((ec_encode_karg<n, EncPol<u, kBufNT, kBufNT, 2>, kEncLUT>), dim3(tiles),         \
+                         dim3(kBlock), 0, s, *a, len, k, tiles, 0ull, 0u);                              \
+    break;
+#define EC_KARG_U(n) EC_KARG(n, 12) EC_KARG(n, 10) EC_KARG(n, 8) EC_KARG(n, 6) EC_KARG(n, 5) EC_KARG(n, 4)
+    EC_KARG_U(1) EC_KARG_U(2) EC_KARG_U(3) EC_KARG_U(4) EC_KARG_U(5) EC_KARG_U(6) EC_KARG_U(7) EC_KARG_U(8)
+#undef EC_KARG_U
+#undef EC_KARG
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
+  isal_hip_count_launch();
+  return static_cast<int>(hipGetLastError());
 }
 
 extern "C" int isal_hip_launch_verify(const uint64_t* d_ptrs, int ptr_stride, int src_idx0,

@@ -251,6 +251,37 @@ isal_hip_xor_rows(int k, int rows, const unsigned char *gftbls, isal_hip_xrows *
         }
 }
 
+void
+isal_hip_enc_masks(int k, int rows, const unsigned char *gftbls, isal_hip_encmask *m)
+{
+        int g, l, j;
+        memset(m, 0, sizeof(*m));
+        if (k < 1 || k > 64 || rows < 1 || isal_hip_knob(ISAL_HIP_KNOB_ENC_XOR) == 0)
+                return;
+        for (g = 0; g * EC_MAX_ROWS_PER_PASS < rows && g < EC_MAX_PASSES; g++) {
+                const int r0 = g * EC_MAX_ROWS_PER_PASS;
+                const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
+                unsigned long long rm = 0;
+                unsigned cm = 0;
+                int good = 1;
+                for (j = 0; j < k && good; j++) {
+                        const unsigned char c = gftbls[((size_t) r0 * k + j) * 32 + 1];
+                        good = c <= 1;
+                        rm |= (unsigned long long) (c & 1) << j;
+                }
+                for (l = 0; l < P && good; l++) {
+                        const unsigned char c = gftbls[((size_t) (r0 + l) * k) * 32 + 1];
+                        good = c <= 1;
+                        cm |= (unsigned) (c & 1) << l;
+                }
+                if (good) {
+                        m->ok |= 1u << g;
+                        m->r0[g] = rm;
+                        m->c0[g] = cm;
+                }
+        }
+}
+
 /* ---- version (reference isal_api.h:93,104) ------------------------------ */
 
 const char *

@@ -38,11 +38,42 @@ unsigned char isal_hip_gf_mul(unsigned char a, unsigned char b);
 void isal_hip_build_tables(int k, int rows, const unsigned char *gftbls, uint32_t *tbl);
 size_t isal_hip_tables_dwords(int k, int rows);
 
+/* 0/1 structure of an encode's coefficient passes. Every gf_gen_rs_matrix
+ * parity block has row 0 = all ones and column 0 = all ones (ec_base.c
+ * gf_gen_rs_matrix: p = 1 for j = 0, gen = 1 for the first parity row); so
+ * does RAID pq_gen's. A product with a 0/1 coefficient is x & mask (one VALU
+ * op per dword, or none when it starts the sum) instead of three v_perm
+ * lookups and their folds. Pass g (rows 8g..8g+P-1) qualifies — bit g of
+ * `ok` — when its first row and its column of source 0 hold only 0 and 1 and
+ * k <= 64; then r0[g] has bit j set where row 8g's coefficient of source j is
+ * 1, and c0[g] bit l where row 8g + l's coefficient of source 0 is 1.
+ * ISAL_HIP_ENC_XOR=0 clears `ok` (every pass takes the lookup path). */
+#define EC_MAX_PASSES 32
+typedef struct {
+        unsigned ok;
+        unsigned c0[EC_MAX_PASSES];
+        unsigned long long r0[EC_MAX_PASSES];
+} isal_hip_encmask;
+void isal_hip_enc_masks(int k, int rows, const unsigned char *gftbls, isal_hip_encmask *m);
+
 /* Kernel launchers (ec_kernels.hip). Return 0 or a hipError_t value.
  * `stream` is a hipStream_t. `vec16` = every shard address is 16-byte aligned. */
 int isal_hip_launch_encode(const uint64_t *d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
                            const uint32_t *d_tbl, int len, int k, int rows, long long nstripes,
-                           int vec16, void *stream);
+                           int vec16, const isal_hip_encmask *em, void *stream);
+/* One stripe of device-resident, 16-byte aligned shards whose pointer table
+ * (k sources then rows outputs) and coefficient tables (one pass: rows <=
+ * EC_MAX_ROWS_PER_PASS, the layout above) travel as 2 KiB of kernel
+ * arguments — no argument upload before the launch. Needs k + rows <=
+ * ISAL_HIP_KARG_PTRS and 5 * k * rows <= ISAL_HIP_KARG_TBL. */
+#define ISAL_HIP_KARG_PTRS 32
+#define ISAL_HIP_KARG_TBL 448
+typedef struct {
+        uint64_t ptrs[ISAL_HIP_KARG_PTRS];
+        uint32_t tbl[ISAL_HIP_KARG_TBL];
+} isal_hip_karg;
+int isal_hip_launch_encode_karg(const isal_hip_karg *a, int len, int k, int rows,
+                                const isal_hip_encmask *em, void *stream);
 int isal_hip_launch_update(const uint64_t *d_ptrs, int ptr_stride, int src_idx, int dst_idx0,
                            const uint32_t *d_tbl, int len, int k, int rows, int vec_i,
                            long long nstripes, int vec16, void *stream);
@@ -120,6 +151,7 @@ enum {
         ISAL_HIP_KNOB_XCD_ORDER,       /* update / CRC kernels: 1 XCD-contiguous items */
         ISAL_HIP_KNOB_ENC_STORE,       /* vector encode stores: 1 sc1 + nt (A/B) | nt */
         ISAL_HIP_KNOB_CRC64_PRE_PIPE,  /* checksum-only CRC64: 1 pipelined lookups (slower; off) */
+        ISAL_HIP_KNOB_ENC_XOR,         /* 0: the encode computes 0/1 rows and columns with lookups too */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

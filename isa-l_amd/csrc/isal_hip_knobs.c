@@ -55,6 +55,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_XCD_ORDER] = {"ISAL_HIP_XCD_ORDER", NULL},
         [ISAL_HIP_KNOB_ENC_STORE] = {"ISAL_HIP_ENC_STORE", NULL},
         [ISAL_HIP_KNOB_CRC64_PRE_PIPE] = {"ISAL_HIP_CRC64_PRE_PIPE", NULL},
+        [ISAL_HIP_KNOB_ENC_XOR] = {"ISAL_HIP_ENC_XOR", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];

@@ -32,6 +32,7 @@ struct isal_hip_pipe {
         unsigned char *d_buf; /* depth x (k + rows) x len */
         uint64_t *d_ptrs;     /* depth x (k + rows) */
         uint32_t *d_tbl;
+        isal_hip_encmask em;   /* 0/1 rows and columns of the coefficients */
         hipEvent_t *src_ready; /* depth x k */
         hipEvent_t *parity_done, *slot_free;
         int *slot_used;
@@ -107,6 +108,7 @@ isal_hip_pipe_create(isal_hip_pipe **out, int len, int k, int rows, const unsign
                 for (i = 0; i < nptr; i++)
                         h_ptrs[i] = (uint64_t) (uintptr_t) (p->d_buf + i * (size_t) len);
                 isal_hip_build_tables(k, rows, gftbls, h_tbl);
+                isal_hip_enc_masks(k, rows, gftbls, &p->em);
                 if (hipMemcpy(p->d_ptrs, h_ptrs, nptr * 8, hipMemcpyHostToDevice) != hipSuccess ||
                     hipMemcpy(p->d_tbl, h_tbl, ntbl * 4, hipMemcpyHostToDevice) != hipSuccess)
                         rc = ISAL_HIP_EHIP;
@@ -165,7 +167,7 @@ isal_hip_pipe_submit(isal_hip_pipe *p, unsigned char *const *data, unsigned char
         }
         if (p->mode == ISAL_HIP_PIPE_ENCODE) {
                 if (isal_hip_launch_encode(ptrs, stride, 0, p->k, p->d_tbl, p->len, p->k, p->rows, 1,
-                                           vec16, p->comp))
+                                           vec16, &p->em, p->comp))
                         return ISAL_HIP_EHIP;
         }
         PIPE_CK(hipEventRecord(p->parity_done[slot], p->comp));

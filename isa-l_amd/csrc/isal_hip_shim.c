@@ -520,7 +520,7 @@ min_slot(const unsigned long long *slots, int n)
  * at args + L->slots_off. */
 static hipError_t
 launch_op(ctx_t *c, int op, char *args, const layout_t *L, int nptr, int nsrc, int clen,
-          long long c0, int k, int rows, int vec_i, int vec16, int *nslots)
+          long long c0, int k, int rows, int vec_i, int vec16, const isal_hip_encmask *em, int *nslots)
 {
         const uint64_t *ptrs = (const uint64_t *) args;
         const uint32_t *tbl = (const uint32_t *) (args + L->ptr_bytes);
@@ -531,7 +531,7 @@ launch_op(ctx_t *c, int op, char *args, const layout_t *L, int nptr, int nsrc, i
                         (unsigned long long *) (args + L->slots_off), nslots, vec16, c->stream);
         if (op == OP_ENCODE)
                 return (hipError_t) isal_hip_launch_encode(ptrs, nptr, 0, nsrc, tbl, clen, k, rows,
-                                                           1, vec16, c->stream);
+                                                           1, vec16, em, c->stream);
         return (hipError_t) isal_hip_launch_update(ptrs, nptr, 0, nsrc, tbl, clen, k, rows, vec_i,
                                                    1, vec16, c->stream);
 }
@@ -598,7 +598,7 @@ fault_at(int site, long long chunk)
 static gpu_res
 gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
           unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
-          int nstage, int zero_copy)
+          int nstage, int zero_copy, const isal_hip_encmask *em)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         int nptr = nsrc + rows, i, s, first_out = -1, vec16 = 1, nslots;
@@ -634,7 +634,7 @@ gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
         }
         if (!zero_copy)
                 GPU_TRY_AT(r, FAULT_H2D, hipMemcpyAsync(c->d_args, h, upload, hipMemcpyHostToDevice, c->stream));
-        GPU_TRY_AT(r, FAULT_LAUNCH, launch_op(c, op, dv, &L, nptr, nsrc, len, 0, k, rows, vec_i, vec16, &nslots));
+        GPU_TRY_AT(r, FAULT_LAUNCH, launch_op(c, op, dv, &L, nptr, nsrc, len, 0, k, rows, vec_i, vec16, em, &nslots));
         if (!zero_copy) {
                 if (op == OP_VERIFY)
                         GPU_TRY(r, hipMemcpyAsync(h + L.slots_off, (char *) c->d_args + L.slots_off,
@@ -709,7 +709,7 @@ job_add(copyjob_t *j, void *dst, const void *src, size_t bytes, hipMemcpyKind ki
 static gpu_res
 gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
             unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
-            int nstage)
+            int nstage, const isal_hip_encmask *em)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         int nptr = nsrc + rows, i, nslots, par = 0;
@@ -804,7 +804,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
                 GPU_TRY(r, hipMemcpyAsync(c->d_args, c->h_args, L.args_bytes,
                                           hipMemcpyHostToDevice, c->stream));
                 GPU_TRY_ATC(r, FAULT_LAUNCH, ci, launch_op(c, op, (char *) c->d_args, &L, nptr, nsrc, clen, c0, k, rows,
-                                     vec_i, vec16, &nslots));
+                                     vec_i, vec16, em, &nslots));
                 if (op == OP_VERIFY) {
                         GPU_TRY(r, hipMemcpyAsync((char *) c->h_args + L.slots_off,
                                                   (char *) c->d_args + L.slots_off,
@@ -1087,7 +1087,7 @@ outq_wait(outq_t *q, long long n)
 static gpu_res
 gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
               unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
-              int nstage)
+              int nstage, const isal_hip_encmask *em)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         const int nptr = nsrc + rows;
@@ -1101,7 +1101,7 @@ gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsig
         if (chunk > per)
                 chunk = per < 4096 ? 4096 : per;
         if (chunk >= (size_t) len) /* one chunk: nothing to overlap */
-                return gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage);
+                return gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, em);
         slot = (chunk + 255) & ~(size_t) 255;
         set_bytes = slot * (size_t) nstage;
         GPU_TRY_AT(r, FAULT_ALLOC, ensure_stage(c, set_bytes * PIPE_NBUF));
@@ -1183,7 +1183,7 @@ gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsig
                 PIPE_STEP(FAULT_NONE, hipStreamWaitEvent(c->stream, c->ev_in[b], 0));
                 PIPE_STEP(FAULT_NONE, hipMemcpyAsync(dargs, h, L.args_bytes, hipMemcpyHostToDevice, c->stream));
                 PIPE_STEP(FAULT_LAUNCH, (hipError_t) launch_op(c, op, dargs, &L, nptr, nsrc, clen, c0, k, rows,
-                                                               vec_i, vec16, &nslots));
+                                                               vec_i, vec16, em, &nslots));
                 PIPE_STEP(FAULT_NONE, hipEventRecord(c->ev_k[b], c->stream));
 #undef PIPE_STEP
                 if (e != hipSuccess) {
@@ -1255,6 +1255,7 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         const int be = backend();
         const int nptr = nsrc + rows;
         uint64_t view_buf[512], *view;
+        isal_hip_encmask em;
         int i, nstage = 0, ndev = 0, all_host, cur_dev;
         size_t bytes;
         gpu_res r;
@@ -1313,6 +1314,10 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 return cpu_route(op, 0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
         }
 
+        if (op == OP_ENCODE)
+                isal_hip_enc_masks(k, rows, gftbls, &em);
+        else
+                em.ok = 0;
         c = ctx_get(&r.err, &r.what);
         if (!c) {
                 r.done = 0;
@@ -1321,14 +1326,14 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 const int zc = bytes <= ZC_BYTES;
                 route_log(op, len, k, rows, zc ? "gpu zero-copy" : "gpu packed",
                           all_host ? "host shards" : "device shards");
-                r = gpu_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, zc);
+                r = gpu_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, zc, &em);
         } else {
                 const int piped = nstage && op != OP_VERIFY && isal_hip_knob(ISAL_HIP_KNOB_PIPE_CHUNKS) != 0;
                 route_log(op, len, k, rows,
                           piped ? "gpu pipelined chunks" : nstage ? "gpu chunked" : "gpu direct (no staging)",
                           all_host ? "host shards" : "device shards");
-                r = piped ? gpu_pipelined(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage)
-                          : gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage);
+                r = piped ? gpu_pipelined(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, &em)
+                          : gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, &em);
         }
         if (view != view_buf)
                 free(view);
@@ -1451,6 +1456,7 @@ struct isal_hip_batch {
         uint64_t *d_ptrs;
         uint32_t *d_tbl;
         isal_hip_xrows xr; /* 0/1 parity rows: CRCs derived, not computed */
+        isal_hip_encmask em; /* 0/1 rows and columns: XORs instead of lookups */
         /* CRC32C state, allocated on first use: kernel tables + combine plan,
          * and the per-lane partials (crc_kernels.hip) */
         isal_hip_crc_geom crc;
@@ -1520,6 +1526,7 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         uint32_t *h;
         hipError_t e;
         isal_hip_xrows xr;
+        isal_hip_encmask em;
         if (!b || !gftbls)
                 return ISAL_HIP_EINVAL;
         n = isal_hip_tables_dwords(b->k, b->rows);
@@ -1530,6 +1537,7 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         /* published with the device tables only: a failed update keeps the
          * old row masks beside the old coefficients */
         isal_hip_xor_rows(b->k, b->rows, gftbls, &xr);
+        isal_hip_enc_masks(b->k, b->rows, gftbls, &em);
         if (!b->d_tbl) {
                 if (hipMalloc((void **) &b->d_tbl, n * 4 + 4) != hipSuccess) {
                         free(h);
@@ -1547,6 +1555,7 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         if (e != hipSuccess)
                 return ISAL_HIP_EHIP;
         b->xr = xr;
+        b->em = em;
         return ISAL_HIP_OK;
 }
 
@@ -1556,7 +1565,7 @@ isal_hip_batch_encode(isal_hip_batch *b, void *stream)
         if (!b)
                 return ISAL_HIP_EINVAL;
         return isal_hip_launch_encode(b->d_ptrs, b->k + b->rows, 0, b->k, b->d_tbl, b->len, b->k,
-                                      b->rows, b->nstripes, b->vec16, stream)
+                                      b->rows, b->nstripes, b->vec16, &b->em, stream)
                        ? ISAL_HIP_EHIP
                        : ISAL_HIP_OK;
 }

@@ -305,7 +305,7 @@ int main(int argc, char** argv) {
   V.push_back({NAME, enc_bytes, [=](hipStream_t st) {                                          \
                  unsigned gr = (GRID) ? std::min<unsigned>((GRID), nitems) : nitems;          \
                  hipLaunchKernelGGL((ec_encode_v16<4, POL>), dim3(gr), dim3(256), 0, st, d_ptrs, \
-                                    stride, 0, k, (const uint32_t*)d_tbl, len, k, nitems, tiles); \
+                                    stride, 0, k, (const uint32_t*)d_tbl, len, k, nitems, tiles, 0ull, 0u); \
                }});                                                                           \
   V.back().encode = true;
   using PNB = Pol<4, true, true, 0>;
@@ -335,7 +335,7 @@ int main(int argc, char** argv) {
   V.push_back({NAME, enc_bytes, [=](hipStream_t st) {                                          \
                  hipLaunchKernelGGL((ec_encode_v16<4, POL>), dim3(nitems), dim3(256), 0, st,     \
                                     d_pptrs[Q], stride, 0, k, (const uint32_t*)d_tbl, len, k,    \
-                                    nitems, tiles);                                            \
+                                    nitems, tiles, 0ull, 0u);                                  \
                }});
   ENCP(PNB, 0, "encode U4 nt-both pad256 (unchecked)")
   ENCP(PNB, 1, "encode U4 nt-both pad4K (unchecked)")

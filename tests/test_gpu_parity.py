@@ -353,6 +353,63 @@ def test_batch_encode_xcd_order_vs_oracle(engine, oracle, gpu, monkeypatch, stor
     b.close()
 
 
+def _coef_01(rng, k, rows, kind):
+    """Coefficient matrices for the encode's 0/1 fast path (isal_hip_encmask):
+    'mask' = random bytes with row 0 and column 0 random 0/1 (the masks
+    matter, not only all-ones), 'rowonly' = row 0 is 0/1 but column 0 is not
+    (the pass falls back to lookups), 'big' = no 0/1 structure at all."""
+    c = rng.integers(2, 256, (rows, k), dtype=np.uint8)
+    if kind in ("mask", "rowonly"):
+        c[0] = rng.integers(0, 2, k, dtype=np.uint8)
+    if kind == "mask":
+        c[:, 0] = rng.integers(0, 2, rows, dtype=np.uint8)
+    return c.reshape(-1)
+
+
+@pytest.mark.parametrize("xor", ["1", "0"])
+@pytest.mark.parametrize("k,rows,n,ns,gen", [
+    (10, 4, 65536 + 48, 9, "rs"),       # C2 shape class, pairs of sources
+    (10, 6, 65536, 8, "rs"),            # P = 6: no pairs
+    (10, 8, 32768 + 16, 5, "rs"),       # P = 8
+    (20, 6, 65536, 4, "rs"),            # two load groups of 10: source 10 starts no sum
+    (12, 9, 16384, 3, "rs"),            # a second pass (row 8): its row 0 is not 0/1
+    (7, 5, 4096 * 3 + 32, 6, "rs"),     # U = 4 with a remainder pair and single
+    (3, 3, 8192, 4, "rs"),              # k < U: every source in the remainder loop
+    (5, 5, 8192, 4, "rs"),              # U = 5 = k
+    (64, 4, 4096, 2, "rs"),             # widest k with masks
+    (65, 3, 4096, 2, "rs"),             # k > 64: no masks, lookups
+    (10, 4, 65536, 5, "mask"), (20, 6, 16384, 3, "mask"), (10, 8, 8192, 3, "mask"),
+    (10, 5, 8192, 3, "rowonly"), (10, 4, 8192, 3, "big"),
+])
+def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, k, rows, n, ns, gen):
+    """Rows and columns of 0/1 coefficients (gf_gen_rs_matrix row 0 and column
+    0, RAID P) take XORs instead of v_perm lookups (ISAL_HIP_ENC_XOR, default
+    on): batch and drop-in encode == oracle with the fast path on and off."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_ENC_XOR", xor)
+    if gen == "rs":
+        coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+    else:
+        coef = _coef_01(np.random.default_rng(k * 131 + rows), k, rows, gen)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 1000 + k + rows)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.encode(0)
+    torch.cuda.synchronize()
+    h_data, h_cod = _host(data), _host(coding)
+    want = _oracle_encode_all(oracle, coef, k, rows, [[h_data[s, j] for j in range(k)] for s in range(ns)])
+    for s in range(ns):
+        for l in range(rows):
+            assert np.array_equal(h_cod[s, l], want[s][l]), (s, l)
+    b.close()
+    # the drop-in call on device shards of the last stripe
+    out = [torch.zeros(n, dtype=torch.uint8, device=gpu) for _ in range(rows)]
+    engine.ec_encode_data(n, k, rows, tbls, [data[ns - 1, j] for j in range(k)], out)
+    for l in range(rows):
+        assert np.array_equal(out[l].cpu().numpy(), want[ns - 1][l]), l
+
+
 def test_xcd_item_order_update_and_checksums(engine, oracle, gpu, monkeypatch):
     """ISAL_HIP_XCD_ORDER=1 (update, checksum-only and fused CRC kernels take
     their items XCD-contiguously): item counts that are multiples of 8 (the

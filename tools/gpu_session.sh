@@ -177,6 +177,18 @@ for s in $STEPS; do
                         run pmc_sq_$tag 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_$tag" -o s -- python3 bench.py $args --steps 2 --warmup 1
                 done
                 ;;
+        xor)
+                # encode 0/1 fast path (ISAL_HIP_ENC_XOR): parity tests, then A/B per shape
+                run pytest_gpu_xor 600 python -u -m pytest tests -m gpu -x -v -k "xor_fast_path or config_c2 or random_shapes or raid or maximum_stripe" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for shape in ${XOR_SHAPES:-10_4_1048576_1024 20_6_4194304_64 10_8_1048576_1024 10_6_1048576_1024}; do
+                                set -- ${shape//_/ }
+                                for x in 0 1; do
+                                        ISAL_HIP_ENC_XOR=$x run bench_k$1p$2_x${x}_r$r 300 python bench.py --workload encode --k $1 --p $2 --len $3 --stripes $4 --no-cpu-baseline
+                                done
+                        done
+                done
+                ;;
         dropin)
                 # the synchronous drop-in call on device-resident C2 stripes, 1/4/16 threads
                 for t in 1 4 16; do
