@@ -355,13 +355,15 @@ __device__ __forceinline__ void dot_bytes(const uint64_t* __restrict__ sp, int s
 // Live VGPRs ~ 4U (loads in flight) + 4P (accumulators) + ~32 (selectors,
 // table halves, addresses); the 512-entry file gives 512/alloc waves per SIMD.
 // The kEncXor variant (FL 1) keeps a source's raw dwords live beside its
-// selectors (row 0 is x & m): 8 more VGPRs; so do P >= 6 and the verify
-// kernel (FL 2, which also holds the stored parity): without them these
-// spilled to scratch (`make -C isa-l_amd isa` reports every kernel's budget).
+// selectors (row 0 is x & m): 8 more VGPRs; the verify kernel (FL 2) also
+// holds the stored parity: 16 more; so do wide passes with small load groups
+// (their remainder loops). Without them these spilled to scratch
+// (`make -C isa-l_amd isa` reports every kernel's budget; a larger budget
+// is not always better: the scheduler then spends it and may spill).
 template <int P, int U, int FL = 0>
 constexpr int enc_waves() {
-  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8 + (FL == 1 ? 8 : 0) + (P >= 6 ? 8 : 0) +
-                      (FL == 2 ? 16 : 0);
+  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8 + (FL == 1 ? 8 : 0) + (FL == 2 ? 16 : 0) +
+                      (P >= 5 && U <= 6 ? (P == 8 && U == 4 ? 32 : 16) : 0);
   constexpr int w = 512 / est;
   return w > 8 ? 8 : (w < 4 ? 4 : w);
 }

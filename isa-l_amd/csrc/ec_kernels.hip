@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encod
   // `a` is the first argument, at offset 0 of the kernarg segment: read it in
   // place (scalar loads) — indexing the by-value copy with runtime indices
   // made the compiler copy all 2 KiB of it to scratch.
-  const auto* ka = reinterpret_cast<const isal_hip_karg*>(__builtin_amdgcn_kernarg_segment_ptr());
+  const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
   encode_items<P, Pol, FL>(ka->ptrs, k + P, 0, k, ka->tbl, len, k, tiles, tiles, r0m, c0m);
 }
 
