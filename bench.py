@@ -59,7 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--len", type=int, default=1 << 20, help="shard bytes")
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU per step")
     ap.add_argument("--workload", choices=["encode", "decode", "update", "encode-crc", "crc", "crc64", "encode-crc64",
-                                           "e2e-update", "e2e-encode", "c1"],
+                                           "e2e-update", "e2e-encode", "c1", "dropin"],
                     default="encode",
                     help="e2e-*: host-resident (pinned) stripes streamed through the pipeline")
     ap.add_argument("--depth", type=int, default=3, help="e2e pipeline depth (stripes in flight)")
@@ -82,6 +82,9 @@ def parse_args(argv=None):
     ap.add_argument("--dist-always", action="store_true",
                     help="initialise the process group even at world size 1 (exercises the RCCL "
                          "control plane on a one-GPU box)")
+    ap.add_argument("--dropin-threads", default="1,4,16",
+                    help="dropin: calling threads per run (tools/dropin_bench), comma-separated")
+    ap.add_argument("--dropin-seconds", type=float, default=3.0, help="dropin: seconds per thread count")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the distributed harness without a GPU (gloo, dummy step)")
     return ap.parse_args(argv)
@@ -798,6 +801,8 @@ def main(argv=None):
         return launch_ranks(args, argv)
     if args.workload == "c1":
         return c1_cpu(args)
+    if args.workload == "dropin":
+        return dropin(args)
     d = Dist(args.dry_run, args.dist_backend, args.dist_always, args.gpus)
     d.topology(args.dry_run)
     if args.dry_run:
@@ -1204,6 +1209,56 @@ def c1_cpu(args):
     }
     print(json.dumps(result), flush=True)
     return 0 if ok_eng else 1
+
+
+def dropin(args):
+    """The drop-in API as a storage caller drives it: one synchronous
+    ec_encode_data per stripe on device-resident shards
+    (erasure_code_perf.c:126-132 calls it in a loop the same way), from
+    1 / 4 / 16 host threads (tools/dropin_bench, a C program linked against
+    libisal_hip.so — no Python in the timed loop; started as a child process
+    before this one touches the GPU). value = GiB/s of (k+p)*len per call at
+    the largest thread count; every run self-checks two stripes' parity
+    against the library's host GF math."""
+    import subprocess
+
+    exe = os.path.join(REPO, "tools", "dropin_bench")
+    if not os.path.exists(exe):
+        raise SystemExit("bench.py: tools/dropin_bench not built (make -C isa-l_amd tools)")
+    k, p, n = args.k, args.p, args.len
+    stripes = min(args.stripes, 64)
+    runs = []
+    for t in [int(x) for x in args.dropin_threads.split(",") if x]:
+        r = subprocess.run([exe, str(k), str(p), str(n), str(stripes), str(t), str(args.dropin_seconds)],
+                           capture_output=True, text=True, timeout=120 + 2 * args.dropin_seconds)
+        if r.returncode != 0:
+            raise SystemExit(f"bench.py: dropin_bench failed ({r.returncode}): {r.stderr[-2000:]}")
+        runs.append(json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1]))
+    top = runs[-1]
+    result = {
+        "metric": "ec_encode_data drop-in GiB/s device-resident, one synchronous call per stripe",
+        "value": round(top["gib_s"], 2),
+        "unit": "GiB/s",
+        "n_gpus": 1,
+        "steps": top["calls"],
+        "warmup": 2 * top["threads"],
+        "ms_per_step": round(top["us_per_call"] / 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "none",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (xorshift bytes copied into HBM; 64 resident stripes cycled)",
+        "config": {"workload": f"drop-in ec_encode_data(len={n}, k={k}, rows={p}) per stripe on hipMalloc'ed "
+                               f"shards, {stripes} stripes, from {top['threads']} host threads",
+                   "k": k, "p": p, "shard_bytes": n},
+        "threads": [{a: r[a] for a in ("threads", "calls", "us_per_call", "calls_per_s", "gib_s", "self_check")}
+                    for r in runs],
+        "self_check": all(r["self_check"] for r in runs),
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    print(json.dumps(result), flush=True)
+    return 0 if result["self_check"] else 1
 
 
 def e2e(args, d: Dist, a, k, p, n):

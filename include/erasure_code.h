@@ -16,10 +16,14 @@
  * (hipMalloc / hipMallocManaged); the engine classifies each pointer
  * (hipPointerGetAttributes) and routes the call (isal_hip.h, "routing"):
  *   - any shard in device memory: GPU kernels;
- *   - all shards in host memory and (k + rows) * len <= 8 MiB: the engine's
- *     CPU route (ec_cpu.c: AVX-512 GFNI affine, else AVX2 nibble shuffles,
- *     else per byte) — below that size the GPU round trip costs more;
- *   - larger host calls: GPU kernels through pinned / HBM staging.
+ *   - all shards in host memory and (k + rows) * len at most a size limit:
+ *     the engine's CPU route (ec_cpu.c: AVX-512 GFNI affine, else AVX2 nibble
+ *     shuffles, else per byte) — below it the GPU round trip costs more. The
+ *     limit is 8 MiB, or 2 MiB when every shard is page-locked and the
+ *     kernels can use it in place (the numbers and knobs: isal_hip.h,
+ *     "routing");
+ *   - larger host calls: GPU kernels, page-locked shards in place, pageable
+ *     ones through HBM staging.
  * A GPU runtime error during a host-resident call is reported once on stderr
  * and the columns not yet final finish on the CPU route, so results are
  * unchanged. A call with any device-resident shard (which no CPU route can

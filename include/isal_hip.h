@@ -184,18 +184,29 @@ void isal_hip_multi_partition(long long nstripes, int ndev, int dev, long long *
 /*
  * The synchronous drop-in calls (erasure_code.h, gf_vect_mul.h, raid.h) route
  * each call by where its shards live and how large it is:
- *   - any device-resident shard: the GPU kernels;
+ *   - any device-resident shard: the GPU kernels. An encode whose shards are
+ *     all device-resident and 16-byte aligned, with k + rows <= 32, rows <= 8
+ *     and k * rows <= 89, passes its shard pointers and coefficient tables as
+ *     kernel arguments: one launch and one stream synchronisation per call
+ *     (ISAL_HIP_KARG=0 uploads them with a copy instead);
  *   - host-resident shards, (k + rows) * len > ISAL_HIP_CPU_MAX_BYTES: the GPU
  *     kernels. Page-locked host shards (hipHostMalloc / hipHostRegister) are
- *     read and written in place through their device mapping (an update's
- *     parity excepted: staged); pageable ones are staged through HBM, in
- *     pipelined 4 MiB column chunks when longer (ISAL_HIP_CHUNK_KB,
- *     ISAL_HIP_PIPE_CHUNKS=0 for one chunk, ISAL_HIP_PINNED_DIRECT=0 to stage
- *     page-locked shards too). Large calls use a per-thread copy-out helper
- *     thread and two extra streams;
+ *     read and written in place through their device mapping when the whole
+ *     shard lies in one registration (an update's parity excepted: staged);
+ *     pageable ones, and page-locked shards that run past their
+ *     registration, are staged through HBM, in pipelined 4 MiB column chunks
+ *     when longer (ISAL_HIP_CHUNK_KB, ISAL_HIP_PIPE_CHUNKS=0 for one chunk,
+ *     ISAL_HIP_PINNED_DIRECT=0 to stage page-locked shards too);
  *   - host-resident shards up to ISAL_HIP_CPU_MAX_BYTES (default 8 MiB; when
  *     every shard is page-locked, ISAL_HIP_CPU_MAX_BYTES_PINNED, default
  *     2 MiB), or a host without a usable GPU: the engine's CPU route.
+ * Per calling thread the library keeps a blocking HIP stream, a pinned
+ * argument buffer and the last call's coefficient tables. A thread that makes
+ * a large staged host call also gets a copy-out helper thread, two more
+ * streams and nine events, kept until the thread exits: at most
+ * ISAL_HIP_MAX_HELPERS (default 8) helpers live in a process — a thread
+ * beyond that issues its copies alone (slower, same result). Streams share
+ * the process's GPU_MAX_HW_QUEUES hardware queues.
  * ISAL_HIP_BACKEND=gpu forces the kernels for every call (and aborts when no
  * GPU is usable), =cpu sends every host-resident call to the CPU route,
  * =auto (default) is the rule above. Routing classifies each shard pointer

@@ -149,9 +149,26 @@ __device__ __forceinline__ uint32_t r0_mask(unsigned long long src, int j) {
 // R0: output row 0's coefficient is 0/1 (mask m0), so row 0 is x & m0 — one
 // op per dword instead of three v_perm lookups (the fused encode+CRC kernels,
 // which are VALU-bound, take it when row 0 is such a row).
-template <int P, bool R0 = false>
+// LT: the low table halves (a0, b0) of each coefficient come from an LDS copy
+// (lt[l] = {a0, b0}, a broadcast ds_read_b64 into VGPRs) instead of SGPRs —
+// a v_perm may read only one SGPR (gfx9 constant bus), so from SGPRs one half
+// needs a v_mov into a VGPR per (source, row): 0.5 VALU op per dword of work.
+template <bool LT>
+__device__ __forceinline__ void low_halves(const Coef& c, const uint2* lt, int l, uint32_t& a0, uint32_t& b0) {
+  if constexpr (LT) {
+    const uint2 v = lt[l];
+    a0 = v.x;
+    b0 = v.y;
+  } else {
+    a0 = c.a0;
+    b0 = c.b0;
+  }
+}
+
+template <int P, bool R0 = false, bool LT = false>
 __device__ __forceinline__ void mac16(uint32_t (&acc)[P][4], const uint4& x,
-                                      const uint32_t* __restrict__ t, uint32_t m0 = 0) {
+                                      const uint32_t* __restrict__ t, uint32_t m0 = 0,
+                                      const uint2* lt = nullptr) {
   const Sel s[4] = {split(x.x), split(x.y), split(x.z), split(x.w)};
   if constexpr (R0) {
     acc[0][0] = xor_and(acc[0][0], x.x, m0);
@@ -162,10 +179,12 @@ __device__ __forceinline__ void mac16(uint32_t (&acc)[P][4], const uint4& x,
 #pragma unroll
   for (int l = R0 ? 1 : 0; l < P; ++l) {
     const Coef c = load_coef(t + l * kTbl);
+    uint32_t a0, b0;
+    low_halves<LT>(c, lt, l, a0, b0);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      const uint32_t v = xor3(acc[l][d], __builtin_amdgcn_perm(c.a1, c.a0, s[d].s0),
-                              __builtin_amdgcn_perm(c.b1, c.b0, s[d].s1));
+      const uint32_t v = xor3(acc[l][d], __builtin_amdgcn_perm(c.a1, a0, s[d].s0),
+                              __builtin_amdgcn_perm(c.b1, b0, s[d].s1));
       acc[l][d] = v ^ __builtin_amdgcn_perm(0u, c.c, s[d].s2);
     }
   }
@@ -173,11 +192,12 @@ __device__ __forceinline__ void mac16(uint32_t (&acc)[P][4], const uint4& x,
 
 // Two sources at once: the six lookups of a (dword, output) fold into the
 // accumulator with three 3-input XORs.
-template <int P, bool R0 = false>
+template <int P, bool R0 = false, bool LT = false>
 __device__ __forceinline__ void mac16x2(uint32_t (&acc)[P][4], const uint4& x, const uint4& y,
                                         const uint32_t* __restrict__ tx,
                                         const uint32_t* __restrict__ ty, uint32_t mx = 0,
-                                        uint32_t my = 0) {
+                                        uint32_t my = 0, const uint2* ltx = nullptr,
+                                        const uint2* lty = nullptr) {
   const Sel sx[4] = {split(x.x), split(x.y), split(x.z), split(x.w)};
   const Sel sy[4] = {split(y.x), split(y.y), split(y.z), split(y.w)};
   if constexpr (R0) {
@@ -190,14 +210,17 @@ __device__ __forceinline__ void mac16x2(uint32_t (&acc)[P][4], const uint4& x, c
   for (int l = R0 ? 1 : 0; l < P; ++l) {
     const Coef a = load_coef(tx + l * kTbl);
     const Coef b = load_coef(ty + l * kTbl);
+    uint32_t aa0, ab0, ba0, bb0;
+    low_halves<LT>(a, ltx, l, aa0, ab0);
+    low_halves<LT>(b, lty, l, ba0, bb0);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       uint32_t v = acc[l][d];
-      v = xor3(v, __builtin_amdgcn_perm(a.a1, a.a0, sx[d].s0),
-               __builtin_amdgcn_perm(a.b1, a.b0, sx[d].s1));
+      v = xor3(v, __builtin_amdgcn_perm(a.a1, aa0, sx[d].s0),
+               __builtin_amdgcn_perm(a.b1, ab0, sx[d].s1));
       v = xor3(v, __builtin_amdgcn_perm(0u, a.c, sx[d].s2),
-               __builtin_amdgcn_perm(b.a1, b.a0, sy[d].s0));
-      v = xor3(v, __builtin_amdgcn_perm(b.b1, b.b0, sy[d].s1),
+               __builtin_amdgcn_perm(b.a1, ba0, sy[d].s0));
+      v = xor3(v, __builtin_amdgcn_perm(b.b1, bb0, sy[d].s1),
                __builtin_amdgcn_perm(0u, b.c, sy[d].s2));
       acc[l][d] = v;
     }
@@ -252,7 +275,9 @@ __device__ __forceinline__ void have_coefs(const Coef (&c)[P]) {
 //            row's sum as x & m (no lookups, no XOR). Masks arrive as kernel
 //            arguments: r0m bit j for row 0's source j, c0m bit l for source
 //            0's row l.
-enum : int { kEncLUT = 0, kEncXor = 1 };
+//   kEncLds  (a bit, with either) the low table halves from an LDS copy
+//            (low_halves), the rest from SGPRs.
+enum : int { kEncLUT = 0, kEncXor = 1, kEncLds = 2 };
 
 // Source pairs share XOR3s but hold two sources' tables in SGPRs (5 dwords per
 // looked-up row each): pairs while at most 4 rows per source are looked up
@@ -260,7 +285,7 @@ enum : int { kEncLUT = 0, kEncXor = 1 };
 // groups of two rows).
 template <int P, int FL>
 constexpr int enc_pair() {
-  return (P - (FL == kEncXor ? 1 : 0)) <= 4 ? 2 : 1;
+  return (P - ((FL & kEncXor) ? 1 : 0)) <= ((FL & kEncLds) ? 8 : 4) ? 2 : 1;
 }
 
 // U sources j..j+U-1: issue all U loads before any arithmetic, then fold the
@@ -273,8 +298,10 @@ constexpr int enc_pair() {
 template <int P, int U, int MODE = kPlain, int FL = kEncLUT>
 __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
                                         int j, long long off, const uint32_t* __restrict__ tbl,
-                                        int len, unsigned long long r0m = 0, unsigned c0m = 0) {
-  constexpr bool X = FL == kEncXor;
+                                        int len, unsigned long long r0m = 0, unsigned c0m = 0,
+                                        const uint2* lt = nullptr) {
+  constexpr bool X = (FL & kEncXor) != 0;
+  constexpr bool LT = (FL & kEncLds) != 0;
   uint4 x[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
@@ -290,7 +317,7 @@ __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* _
         acc[l][3] = x[0].w & m;
       }
     } else {
-      mac16<P, true>(acc, x[0], tbl + j * P * kTbl, r0_mask(r0m, j));
+      mac16<P, true, LT>(acc, x[0], tbl + j * P * kTbl, r0_mask(r0m, j), lt + j * P);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -298,14 +325,16 @@ __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* _
 #pragma unroll
   for (int u = U0; u + PAIR <= U; u += PAIR) {
     if constexpr (PAIR == 2)
-      mac16x2<P, X>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl,
-                    X ? r0_mask(r0m, j + u) : 0u, X ? r0_mask(r0m, j + u + 1) : 0u);
+      mac16x2<P, X, LT>(acc, x[u], x[u + 1], tbl + (j + u) * P * kTbl, tbl + (j + u + 1) * P * kTbl,
+                        X ? r0_mask(r0m, j + u) : 0u, X ? r0_mask(r0m, j + u + 1) : 0u,
+                        lt + (j + u) * P, lt + (j + u + 1) * P);
     else
-      mac16<P, X>(acc, x[u], tbl + (j + u) * P * kTbl, X ? r0_mask(r0m, j + u) : 0u);
+      mac16<P, X, LT>(acc, x[u], tbl + (j + u) * P * kTbl, X ? r0_mask(r0m, j + u) : 0u, lt + (j + u) * P);
     __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (PAIR == 2 && ((U - U0) & 1)) {
-    mac16<P, X>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl, X ? r0_mask(r0m, j + U - 1) : 0u);
+    mac16<P, X, LT>(acc, x[U - 1], tbl + (j + U - 1) * P * kTbl, X ? r0_mask(r0m, j + U - 1) : 0u,
+                    lt + (j + U - 1) * P);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -354,17 +383,21 @@ __device__ __forceinline__ void dot_bytes(const uint64_t* __restrict__ sp, int s
 // Waves per SIMD the register allocator must allow (VGPR budget 512/waves).
 // Live VGPRs ~ 4U (loads in flight) + 4P (accumulators) + ~32 (selectors,
 // table halves, addresses); the 512-entry file gives 512/alloc waves per SIMD.
-// The kEncXor variant (FL 1) keeps a source's raw dwords live beside its
-// selectors (row 0 is x & m): 8 more VGPRs; the verify kernel (FL 2) also
+// The kEncXor variant (FL bit 0) keeps a source's raw dwords live beside its
+// selectors (row 0 is x & m): 8 more VGPRs; the verify kernel (FL 16) also
 // holds the stored parity: 16 more; so do wide passes with small load groups
 // (their remainder loops). Without them these spilled to scratch
 // (`make -C isa-l_amd isa` reports every kernel's budget; a larger budget
 // is not always better: the scheduler then spends it and may spill).
 template <int P, int U, int FL = 0>
 constexpr int enc_waves() {
-  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8 + (FL == 1 ? 8 : 0) + (FL == 2 ? 16 : 0) +
+  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8 + ((FL & 1) ? 8 : 0) + (FL == 16 ? 16 : 0) +
                       (P >= 5 && U <= 6 ? (P == 8 && U == 4 ? 32 : 16) : 0);
-  constexpr int w = 512 / est;
+  constexpr int w = 512 / (est + ((FL & kEncLds) ? 16 : 0));
+  // kEncLds pairs every pass: two sources' low halves of every row in VGPRs;
+  // wide passes get 3 waves' worth (VALU-bound: 12 waves per CU still keep
+  // ~120 KB of loads in flight, twice what the HBM latency needs)
+  if constexpr ((FL & kEncLds) && P >= 5) return 3;
   return w > 8 ? 8 : (w < 4 ? 4 : w);
 }
 
@@ -372,20 +405,21 @@ constexpr int enc_waves() {
 template <int P, class Pol, int FL = kEncLUT>
 __device__ __forceinline__ void accum16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ src,
                                         const uint32_t* __restrict__ tbl, int k, long long off,
-                                        int len, unsigned long long r0m = 0, unsigned c0m = 0) {
+                                        int len, unsigned long long r0m = 0, unsigned c0m = 0,
+                                        const uint2* lt = nullptr) {
 #pragma unroll
   for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
   int j = 0;
-  for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m);
+  for (; j + Pol::U <= k; j += Pol::U) chunk16<P, Pol::U, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m, lt);
   // Remainder. The launcher only picks U > 4 when U divides k, so there the
   // (cheap, correct for any k) single-source loop is dead in practice.
   if constexpr (Pol::U == 4) {
     if (j + 2 <= k) {
-      chunk16<P, 2, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m);
+      chunk16<P, 2, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m, lt);
       j += 2;
     }
   }
-  for (; j < k; ++j) chunk16<P, 1, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m);
+  for (; j < k; ++j) chunk16<P, 1, Pol::LD, FL>(acc, src, j, off, tbl, len, r0m, c0m, lt);
 }
 
 }  // namespace

@@ -39,6 +39,11 @@ __device__ __forceinline__ void encode_items(const uint64_t* __restrict__ ptrs, 
                                              unsigned nitems, unsigned tiles, unsigned long long r0m,
                                              unsigned c0m) {
   const unsigned nstripes = nitems / tiles;
+  extern __shared__ uint2 enc_lt[];  // kEncLds: {a0, b0} of every coefficient of the pass
+  if constexpr ((FL & kEncLds) != 0) {
+    for (int i = threadIdx.x; i < k * P; i += kBlock) enc_lt[i] = make_uint2(tbl[i * kTbl], tbl[i * kTbl + 2]);
+    __syncthreads();
+  }
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     unsigned stripe, tile;
     if constexpr (Pol::ORDER == 0) {
@@ -68,7 +73,7 @@ __device__ __forceinline__ void encode_items(const uint64_t* __restrict__ ptrs, 
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
       uint32_t acc[P][4];
-      accum16<P, Pol, FL>(acc, sp + src0, tbl, k, off, len, r0m, c0m);
+      accum16<P, Pol, FL>(acc, sp + src0, tbl, k, off, len, r0m, c0m, enc_lt);
 #pragma unroll
       for (int l = 0; l < P; ++l)
         store16<Pol::ST>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]),
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(kBlock) void ec_encode_b1(const uint64_t* __restric
 // is reduced into *bad with atomicMin. Nothing is written to the shards.
 // ---------------------------------------------------------------------------
 template <int P>
-__global__ __launch_bounds__(kBlock, (enc_waves<P, 4, 2>())) void ec_verify_v16(
+__global__ __launch_bounds__(kBlock, (enc_waves<P, 4, 16>())) void ec_verify_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles,
     unsigned long long* __restrict__ slots, int row0, long long col0) {
@@ -282,8 +287,18 @@ bool enc_store_sc1() {
   return isal_hip_knob(ISAL_HIP_KNOB_ENC_STORE) == 1;
 }
 
-// XOR fast path (isal_hip_encmask) only in the default policy: XCD-contiguous
-// order, nt buffer loads and stores.
+// Low table halves from LDS (kEncLds; ISAL_HIP_ENC_LDS=0: from SGPRs).
+bool enc_lds() {
+  return isal_hip_knob(ISAL_HIP_KNOB_ENC_LDS) != 0;
+}
+
+template <int P>
+size_t lds_bytes(int k) {
+  return static_cast<size_t>(k) * P * sizeof(uint2);
+}
+
+// XOR fast path (isal_hip_encmask) and LDS table halves only in the default
+// policy: XCD-contiguous order, nt buffer loads and stores.
 template <int P, int U>
 void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
                 int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles,
@@ -291,6 +306,13 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
   if (enc_order() == 2 && enc_store_sc1())
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufSC1NT, 2>>), dim3(grid), dim3(kBlock), 0, s,
                        ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
+  else if (enc_order() == 2 && enc_lds() && x)
+    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncXor | kEncLds>), dim3(grid),
+                       dim3(kBlock), lds_bytes<P>(k), s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems,
+                       tiles, r0m, c0m);
+  else if (enc_order() == 2 && enc_lds())
+    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncLds>), dim3(grid), dim3(kBlock),
+                       lds_bytes<P>(k), s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
   else if (enc_order() == 2 && x)
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncXor>), dim3(grid), dim3(kBlock), 0,
                        s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);

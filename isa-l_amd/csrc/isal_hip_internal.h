@@ -152,9 +152,14 @@ enum {
         ISAL_HIP_KNOB_ENC_STORE,       /* vector encode stores: 1 sc1 + nt (A/B) | nt */
         ISAL_HIP_KNOB_CRC64_PRE_PIPE,  /* checksum-only CRC64: 1 pipelined lookups (slower; off) */
         ISAL_HIP_KNOB_ENC_XOR,         /* 0: the encode computes 0/1 rows and columns with lookups too */
+        ISAL_HIP_KNOB_ENC_LDS,         /* 0: the encode's low table halves from SGPRs (v_mov), not LDS */
+        ISAL_HIP_KNOB_KARG,            /* 0: device-resident drop-in encodes upload their arguments */
+        ISAL_HIP_KNOB_MAX_HELPERS,     /* copy-out helper threads per process (default 8) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);
+/* bumped by every isal_hip_config_reload(): caches derived from knobs check it */
+unsigned isal_hip_knob_generation(void);
 
 /* ---- the host (CPU) route (ec_cpu.c) ---------------------------------------
  * Same ops and return value as isal_hip_run, over HOST-resident shards only,

@@ -56,6 +56,9 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_ENC_STORE] = {"ISAL_HIP_ENC_STORE", NULL},
         [ISAL_HIP_KNOB_CRC64_PRE_PIPE] = {"ISAL_HIP_CRC64_PRE_PIPE", NULL},
         [ISAL_HIP_KNOB_ENC_XOR] = {"ISAL_HIP_ENC_XOR", NULL},
+        [ISAL_HIP_KNOB_ENC_LDS] = {"ISAL_HIP_ENC_LDS", NULL},
+        [ISAL_HIP_KNOB_KARG] = {"ISAL_HIP_KARG", NULL},
+        [ISAL_HIP_KNOB_MAX_HELPERS] = {"ISAL_HIP_MAX_HELPERS", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];
@@ -91,9 +94,18 @@ isal_hip_knob(int id)
         return id >= 0 && id < ISAL_HIP_KNOB_COUNT ? values[id] : -1;
 }
 
+static unsigned generation;
+
 void
 isal_hip_config_reload(void)
 {
         pthread_once(&once, load);
         load();
+        __atomic_add_fetch(&generation, 1u, __ATOMIC_RELEASE);
+}
+
+unsigned
+isal_hip_knob_generation(void)
+{
+        return __atomic_load_n(&generation, __ATOMIC_ACQUIRE);
 }

@@ -88,20 +88,24 @@ isal_hip_numa_node_cpus(const char *root, int node, int *cpus, int max)
         fclose(f);
         if (!p)
                 return -1;
-        /* "0-63,128-191" */
+        /* "0-63,128-191"; CPU numbers at or above CPU_SETSIZE (or a total
+         * beyond it) mark the file malformed: every range is bounded, so a
+         * hostile tree (ISAL_HIP_SYSFS_ROOT) cannot make this loop run away */
         while (*p && *p != '\n') {
                 char *end;
                 long lo = strtol(p, &end, 10), hi;
-                if (end == p || lo < 0)
+                if (end == p || lo < 0 || lo >= CPU_SETSIZE)
                         return -1;
                 hi = lo;
                 p = end;
                 if (*p == '-') {
                         hi = strtol(p + 1, &end, 10);
-                        if (end == p + 1 || hi < lo)
+                        if (end == p + 1 || hi < lo || hi >= CPU_SETSIZE)
                                 return -1;
                         p = end;
                 }
+                if (n > CPU_SETSIZE - (int) (hi - lo + 1))
+                        return -1;
                 for (; lo <= hi; lo++) {
                         if (n < max)
                                 cpus[n] = (int) lo;

@@ -207,6 +207,14 @@ typedef struct {
         int pipe_ready;
         struct outq *oq; /* the call thread's copy-out worker (gpu_pipelined) */
         struct copyjob *jobs; /* [3]: worker's copies in / out, this thread's list */
+        /* the last call's derived coefficient tables and 0/1 masks, reused
+         * while its coefficients (byte 1 of each gftbls entry) repeat */
+        int tk, trows;
+        unsigned tgen;
+        unsigned char *tcoef;
+        uint32_t *ttbl;
+        size_t tcap_coef, tcap_tbl;
+        isal_hip_encmask tem;
 } ctx_t;
 
 /* Copy-out worker of a calling thread. The runtime serves a copy from or to
@@ -278,6 +286,8 @@ ctx_release(void *p)
         if (c->oq)
                 outq_stop(c);
         free(c->jobs);
+        free(c->tcoef);
+        free(c->ttbl);
         if (c->pipe_ready) {
                 int b;
                 (void) hipStreamDestroy(c->s_in);
@@ -335,6 +345,47 @@ ctx_get(hipError_t *err, const char **what)
                 pthread_setspecific(ctx_key, c);
         }
         return c;
+}
+
+/* The call's device coefficient tables (isal_hip_build_tables layout) and 0/1
+ * masks: rebuilt only when the coefficients differ from the thread's last
+ * call (a storage caller encodes stripe after stripe with one matrix; the
+ * rebuild is ~5k table lookups for k = 10, p = 4). NULL when out of memory. */
+static const uint32_t *
+ctx_tables(ctx_t *c, int k, int rows, const unsigned char *gftbls, const isal_hip_encmask **em)
+{
+        const size_t n = (size_t) k * (size_t) rows, nd = isal_hip_tables_dwords(k, rows);
+        const unsigned gen = isal_hip_knob_generation();
+        size_t i;
+        int hit = c->ttbl && c->tk == k && c->trows == rows && c->tgen == gen;
+        for (i = 0; hit && i < n; i++)
+                hit = c->tcoef[i] == gftbls[i * 32 + 1];
+        if (!hit) {
+                if (n > c->tcap_coef) {
+                        unsigned char *x = (unsigned char *) realloc(c->tcoef, n);
+                        if (!x)
+                                return NULL;
+                        c->tcoef = x;
+                        c->tcap_coef = n;
+                }
+                if (nd > c->tcap_tbl) {
+                        uint32_t *x = (uint32_t *) realloc(c->ttbl, nd * 4);
+                        if (!x)
+                                return NULL;
+                        c->ttbl = x;
+                        c->tcap_tbl = nd;
+                }
+                c->tk = -1; /* not valid until rebuilt */
+                for (i = 0; i < n; i++)
+                        c->tcoef[i] = gftbls[i * 32 + 1];
+                isal_hip_build_tables(k, rows, gftbls, c->ttbl);
+                isal_hip_enc_masks(k, rows, gftbls, &c->tem);
+                c->tk = k;
+                c->trows = rows;
+                c->tgen = gen;
+        }
+        *em = &c->tem;
+        return c->ttbl;
 }
 
 static hipError_t
@@ -427,15 +478,23 @@ stage_limit(void)
  * memory: the pointer itself. Page-locked host memory (hipHostMalloc,
  * hipHostRegister — NIC / disk DMA buffers usually are): the device's mapping
  * of it, so kernels read and write it in place over PCIe with no staging copy
- * (ISAL_HIP_PINNED_DIRECT=0 stages it like pageable memory). Pageable
- * memory: 0 — it must be copied through a staging buffer. *is_dev tells
- * device memory (which no CPU route can read) from host memory. */
+ * (ISAL_HIP_PINNED_DIRECT=0 stages it like pageable memory) — but only when
+ * the shard's LAST byte maps through the same registration too: a shard that
+ * runs past the end of a partly registered buffer would make the kernel
+ * touch unmapped memory (a GPU fault the CPU route could not recover from),
+ * so it is staged. Pageable memory: 0 — it must be copied through a staging
+ * buffer. *kind: CL_HOST (pageable or page-locked host memory), CL_DEVICE
+ * (hipMalloc memory: *rbase / *rsize receive its allocation's range) or
+ * CL_MANAGED — device-visible memory that no CPU route can read. */
+enum { CL_HOST = 0, CL_DEVICE = 1, CL_MANAGED = 2 };
+
 static uint64_t
-classify(const void *p, int dev, int *is_dev)
+classify(const void *p, size_t len, int dev, int *kind, uintptr_t *rbase, size_t *rsize)
 {
-        hipPointerAttribute_t a;
+        hipPointerAttribute_t a, z;
         hipError_t e;
-        *is_dev = 0;
+        *kind = CL_HOST;
+        *rsize = 0;
         if (!p)
                 return 0;
         e = hipPointerGetAttributes(&a, p);
@@ -443,9 +502,20 @@ classify(const void *p, int dev, int *is_dev)
                 (void) hipGetLastError(); /* unknown to HIP: plain host memory */
                 return 0;
         }
-        if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
-            a.type == hipMemoryTypeUnified) {
-                *is_dev = 1;
+        if (a.type == hipMemoryTypeDevice) {
+                hipDeviceptr_t base;
+                size_t size;
+                *kind = CL_DEVICE;
+                if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t) p) == hipSuccess) {
+                        *rbase = (uintptr_t) base;
+                        *rsize = size;
+                } else {
+                        (void) hipGetLastError();
+                }
+                return (uint64_t) (uintptr_t) p;
+        }
+        if (a.type == hipMemoryTypeManaged || a.type == hipMemoryTypeUnified) {
+                *kind = CL_MANAGED;
                 return (uint64_t) (uintptr_t) p;
         }
         if (a.type == hipMemoryTypeHost && a.devicePointer && a.device == dev &&
@@ -454,9 +524,50 @@ classify(const void *p, int dev, int *is_dev)
                  * base plus p's offset into it). Only the mapping made for the
                  * calling thread's device is used; page-locked memory of
                  * another device is staged. */
+                const char *last = (const char *) p + (len ? len - 1 : 0);
+                if (len > 1) {
+                        if (hipPointerGetAttributes(&z, last) != hipSuccess) {
+                                (void) hipGetLastError();
+                                return 0;
+                        }
+                        if (z.type != hipMemoryTypeHost || z.device != dev ||
+                            (const char *) z.devicePointer != (const char *) a.devicePointer + (len - 1))
+                                return 0;
+                }
                 return (uint64_t) (uintptr_t) a.devicePointer;
         }
         return 0;
+}
+
+/* Device allocations already seen by one call: a shard inside one of them is
+ * device memory too, with no HIP query (a stripe's shards usually come from
+ * one or two allocations: 14 queries of ~0.4 us become one or two). Only
+ * within one call — a later call may find the memory freed and reused. */
+#define SEEN_MAX 4
+typedef struct {
+        int n;
+        uintptr_t lo[SEEN_MAX], hi[SEEN_MAX];
+} seen_t;
+
+static int
+seen_has(const seen_t *sn, const void *p, size_t len)
+{
+        const uintptr_t a = (uintptr_t) p;
+        int i;
+        for (i = 0; i < sn->n; i++)
+                if (a >= sn->lo[i] && a < sn->hi[i] && len <= sn->hi[i] - a)
+                        return 1;
+        return 0;
+}
+
+static void
+seen_add(seen_t *sn, uintptr_t base, size_t size)
+{
+        if (size && sn->n < SEEN_MAX) {
+                sn->lo[sn->n] = base;
+                sn->hi[sn->n] = base + size;
+                sn->n++;
+        }
 }
 
 /* ---- the generic synchronous call --------------------------------------- */
@@ -598,7 +709,7 @@ fault_at(int site, long long chunk)
 static gpu_res
 gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
           unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
-          int nstage, int zero_copy, const isal_hip_encmask *em)
+          int nstage, int zero_copy, const uint32_t *tbl, const isal_hip_encmask *em)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         int nptr = nsrc + rows, i, s, first_out = -1, vec16 = 1, nslots;
@@ -611,7 +722,7 @@ gpu_small(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned 
         h = (char *) c->h_args;
         dv = zero_copy ? (char *) c->h_args_dev : (char *) c->d_args; /* what kernels see */
         h_ptrs = (uint64_t *) h;
-        isal_hip_build_tables(k, rows, gftbls, (uint32_t *) (h + L.ptr_bytes));
+        memcpy(h + L.ptr_bytes, tbl, isal_hip_tables_dwords(k, rows) * 4);
         upload = L.args_bytes;
         for (i = 0, s = 0; i < nptr; i++) {
                 unsigned char *host = i < nsrc ? src[i] : dst[i - nsrc];
@@ -709,7 +820,7 @@ job_add(copyjob_t *j, void *dst, const void *src, size_t bytes, hipMemcpyKind ki
 static gpu_res
 gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
             unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
-            int nstage, const isal_hip_encmask *em)
+            int nstage, const uint32_t *tbl, const isal_hip_encmask *em)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         int nptr = nsrc + rows, i, nslots, par = 0;
@@ -747,7 +858,7 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
         L = call_layout(op, len, k, rows, nptr, 0);
         GPU_TRY(r, ensure_args(c, L.stage_off));
         h_ptrs = (uint64_t *) c->h_args;
-        isal_hip_build_tables(k, rows, gftbls, (uint32_t *) ((char *) c->h_args + L.ptr_bytes));
+        memcpy((char *) c->h_args + L.ptr_bytes, tbl, isal_hip_tables_dwords(k, rows) * 4);
 
         for (c0 = 0; c0 < len; c0 += (long long) chunk) {
                 int clen = (int) ((long long) len - c0 < (long long) chunk ? len - c0 : (long long) chunk);
@@ -1020,15 +1131,34 @@ outq_main(void *arg)
         return NULL;
 }
 
+/* Copy-out helpers alive in the process, at most max_helpers(): each is a
+ * thread with two streams of its own, and they all share the process's few
+ * hardware queues (isal_hip.h, "routing"). */
+static int g_helpers;
+#define DEFAULT_MAX_HELPERS 8
+
+static int
+max_helpers(void)
+{
+        const long long v = isal_hip_knob(ISAL_HIP_KNOB_MAX_HELPERS);
+        return v >= 0 ? (int) v : DEFAULT_MAX_HELPERS;
+}
+
 static hipError_t
 outq_start(ctx_t *c)
 {
         outq_t *q;
         if (c->oq)
                 return hipSuccess;
+        if (__atomic_add_fetch(&g_helpers, 1, __ATOMIC_ACQ_REL) > max_helpers()) {
+                __atomic_sub_fetch(&g_helpers, 1, __ATOMIC_ACQ_REL);
+                return hipErrorNotSupported; /* over the cap: issue copies alone */
+        }
         q = (outq_t *) calloc(1, sizeof(*q));
-        if (!q)
+        if (!q) {
+                __atomic_sub_fetch(&g_helpers, 1, __ATOMIC_ACQ_REL);
                 return hipErrorOutOfMemory;
+        }
         pthread_mutex_init(&q->mu, NULL);
         pthread_cond_init(&q->cv, NULL);
         c->oq = q;
@@ -1037,6 +1167,7 @@ outq_start(ctx_t *c)
                 pthread_cond_destroy(&q->cv);
                 free(q);
                 c->oq = NULL;
+                __atomic_sub_fetch(&g_helpers, 1, __ATOMIC_ACQ_REL);
                 return hipErrorOutOfMemory;
         }
         return hipSuccess;
@@ -1055,6 +1186,7 @@ outq_stop(ctx_t *c)
         pthread_cond_destroy(&q->cv);
         free(q);
         c->oq = NULL;
+        __atomic_sub_fetch(&g_helpers, 1, __ATOMIC_ACQ_REL);
 }
 
 /* Wait until the worker has enqueued the copies of chunks [0, n) or failed;
@@ -1087,7 +1219,7 @@ outq_wait(outq_t *q, long long n)
 static gpu_res
 gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
               unsigned char *const *src, int nsrc, unsigned char *const *dst, const uint64_t *view,
-              int nstage, const isal_hip_encmask *em)
+              int nstage, const uint32_t *tbl, const isal_hip_encmask *em)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         const int nptr = nsrc + rows;
@@ -1101,7 +1233,13 @@ gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsig
         if (chunk > per)
                 chunk = per < 4096 ? 4096 : per;
         if (chunk >= (size_t) len) /* one chunk: nothing to overlap */
-                return gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, em);
+                return gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, tbl, em);
+        if (!c->oq && outq_start(c) != hipSuccess) {
+                /* no helper for this thread (the process cap, or no thread):
+                 * one chunk at a time, copies issued by this thread alone */
+                (void) hipGetLastError();
+                return gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, tbl, em);
+        }
         slot = (chunk + 255) & ~(size_t) 255;
         set_bytes = slot * (size_t) nstage;
         GPU_TRY_AT(r, FAULT_ALLOC, ensure_stage(c, set_bytes * PIPE_NBUF));
@@ -1111,7 +1249,7 @@ gpu_pipelined(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsig
         astride = (L.args_bytes + 255) & ~(size_t) 255;
         GPU_TRY_AT(r, FAULT_ALLOC, ensure_args(c, astride * PIPE_NBUF));
         /* one argument region per staging set: pointer table + coefficient tables */
-        isal_hip_build_tables(k, rows, gftbls, (uint32_t *) ((char *) c->h_args + L.ptr_bytes));
+        memcpy((char *) c->h_args + L.ptr_bytes, tbl, isal_hip_tables_dwords(k, rows) * 4);
         for (b = 1; b < PIPE_NBUF; b++)
                 memcpy((char *) c->h_args + b * astride + L.ptr_bytes, (char *) c->h_args + L.ptr_bytes,
                        L.args_bytes - L.ptr_bytes);
@@ -1233,6 +1371,37 @@ quiesce(ctx_t *c)
         return e;
 }
 
+/* Kernel-argument encode (isal_hip_launch_encode_karg): one launch, no
+ * argument upload — for device-resident, 16-byte aligned shards of a
+ * one-pass stripe that fits the 2 KiB argument block. */
+static int
+karg_fits(int len, int k, int rows, const uint64_t *view, int nptr)
+{
+        int i;
+        if (len < 16 || rows > EC_MAX_ROWS_PER_PASS || nptr > ISAL_HIP_KARG_PTRS ||
+            isal_hip_tables_dwords(k, rows) > ISAL_HIP_KARG_TBL || isal_hip_knob(ISAL_HIP_KNOB_KARG) == 0)
+                return 0;
+        for (i = 0; i < nptr; i++)
+                if (view[i] & 15)
+                        return 0;
+        return 1;
+}
+
+static gpu_res
+gpu_karg(ctx_t *c, int len, int k, int rows, const uint64_t *view, const uint32_t *tbl,
+         const isal_hip_encmask *em)
+{
+        gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
+        isal_hip_karg a;
+        memset(&a, 0, sizeof(a));
+        memcpy(a.ptrs, view, sizeof(uint64_t) * (size_t) (k + rows));
+        memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
+        GPU_TRY_AT(r, FAULT_LAUNCH, (hipError_t) isal_hip_launch_encode_karg(&a, len, k, rows, em, c->stream));
+        GPU_TRY_AT(r, FAULT_SYNC, hipStreamSynchronize(c->stream));
+        r.done = len;
+        return r;
+}
+
 static unsigned long long
 cpu_route(int op, long long c0, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
           unsigned char *const *src, int nsrc, unsigned char *const *dst)
@@ -1255,7 +1424,10 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         const int be = backend();
         const int nptr = nsrc + rows;
         uint64_t view_buf[512], *view;
-        isal_hip_encmask em;
+        static const isal_hip_encmask no_masks;
+        const isal_hip_encmask *em = &no_masks;
+        const uint32_t *tbl = NULL;
+        seen_t sn;
         int i, nstage = 0, ndev = 0, all_host, cur_dev;
         size_t bytes;
         gpu_res r;
@@ -1290,10 +1462,20 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 (void) hipGetLastError();
                 cur_dev = -1; /* no page-locked shard is used in place */
         }
+        sn.n = 0;
         for (i = 0; i < nptr; i++) {
                 const void *p = i < nsrc ? src[i] : dst[i - nsrc];
-                int is_dev;
-                view[i] = classify(p, cur_dev, &is_dev);
+                int is_dev, kind = CL_DEVICE;
+                uintptr_t rb = 0;
+                size_t rs = 0;
+                if (seen_has(&sn, p, (size_t) len)) {
+                        view[i] = (uint64_t) (uintptr_t) p;
+                } else {
+                        view[i] = classify(p, (size_t) len, cur_dev, &kind, &rb, &rs);
+                        if (kind == CL_DEVICE)
+                                seen_add(&sn, rb, rs);
+                }
+                is_dev = kind != CL_HOST;
                 /* An update's parity in page-locked host memory is staged, not
                  * written in place: a kernel that failed after it started could
                  * have folded some of it already, and the CPU fallback could not
@@ -1314,26 +1496,32 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 return cpu_route(op, 0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
         }
 
-        if (op == OP_ENCODE)
-                isal_hip_enc_masks(k, rows, gftbls, &em);
-        else
-                em.ok = 0;
         c = ctx_get(&r.err, &r.what);
+        if (c && !(tbl = ctx_tables(c, k, rows, gftbls, &em))) {
+                r.err = hipErrorOutOfMemory;
+                r.what = "ctx_tables (host memory)";
+                c = NULL;
+        }
+        if (c && op != OP_ENCODE)
+                em = &no_masks;
         if (!c) {
                 r.done = 0;
                 r.first_bad = ~0ull;
+        } else if (ndev == nptr && op == OP_ENCODE && karg_fits(len, k, rows, view, nptr)) {
+                route_log(op, len, k, rows, "gpu kernel-args", "device shards");
+                r = gpu_karg(c, len, k, rows, view, tbl, em);
         } else if (bytes <= ZC_BYTES || (nstage && (size_t) len * (size_t) nstage <= PACK_BYTES)) {
                 const int zc = bytes <= ZC_BYTES;
                 route_log(op, len, k, rows, zc ? "gpu zero-copy" : "gpu packed",
                           all_host ? "host shards" : "device shards");
-                r = gpu_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, zc, &em);
+                r = gpu_small(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, zc, tbl, em);
         } else {
                 const int piped = nstage && op != OP_VERIFY && isal_hip_knob(ISAL_HIP_KNOB_PIPE_CHUNKS) != 0;
                 route_log(op, len, k, rows,
                           piped ? "gpu pipelined chunks" : nstage ? "gpu chunked" : "gpu direct (no staging)",
                           all_host ? "host shards" : "device shards");
-                r = piped ? gpu_pipelined(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, &em)
-                          : gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, &em);
+                r = piped ? gpu_pipelined(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, tbl, em)
+                          : gpu_chunked(c, op, len, k, rows, vec_i, gftbls, src, nsrc, dst, view, nstage, tbl, em);
         }
         if (view != view_buf)
                 free(view);

@@ -150,6 +150,12 @@ def test_numa_lookup_against_a_faked_sysfs(engine, tmp_path):
     (root / "devices" / "system" / "node" / "node2").mkdir()
     (root / "devices" / "system" / "node" / "node2" / "cpulist").write_text("3-1\n")
     assert engine.numa_node_cpus(2, r) is None  # malformed range
+    # hostile ranges end at once (CPU numbers beyond CPU_SETSIZE are malformed)
+    for bad in ("0-9223372036854775807\n", "5-100000\n", "0-1023,0-1023,0-1023\n", "99999999999999999999\n"):
+        (root / "devices" / "system" / "node" / "node2" / "cpulist").write_text(bad)
+        assert engine.numa_node_cpus(2, r) is None, bad
+    (root / "devices" / "system" / "node" / "node2" / "cpulist").write_text("0-1023\n")
+    assert engine.numa_node_cpus(2, r) == list(range(1024))
     # the real tree of this host parses (node 0 exists on every Linux box with NUMA)
     if os.path.exists("/sys/devices/system/node/node0/cpulist"):
         assert engine.numa_node_cpus(0, None)

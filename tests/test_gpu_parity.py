@@ -366,7 +366,7 @@ def _coef_01(rng, k, rows, kind):
     return c.reshape(-1)
 
 
-@pytest.mark.parametrize("xor", ["1", "0"])
+@pytest.mark.parametrize("xor,lds", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
 @pytest.mark.parametrize("k,rows,n,ns,gen", [
     (10, 4, 65536 + 48, 9, "rs"),       # C2 shape class, pairs of sources
     (10, 6, 65536, 8, "rs"),            # P = 6: no pairs
@@ -381,13 +381,15 @@ def _coef_01(rng, k, rows, kind):
     (10, 4, 65536, 5, "mask"), (20, 6, 16384, 3, "mask"), (10, 8, 8192, 3, "mask"),
     (10, 5, 8192, 3, "rowonly"), (10, 4, 8192, 3, "big"),
 ])
-def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, k, rows, n, ns, gen):
+def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, lds, k, rows, n, ns, gen):
     """Rows and columns of 0/1 coefficients (gf_gen_rs_matrix row 0 and column
-    0, RAID P) take XORs instead of v_perm lookups (ISAL_HIP_ENC_XOR, default
-    on): batch and drop-in encode == oracle with the fast path on and off."""
+    0, RAID P) take XORs instead of v_perm lookups (ISAL_HIP_ENC_XOR), and the
+    low table halves come from LDS (ISAL_HIP_ENC_LDS), both default on: batch
+    and drop-in encode == oracle with each on and off."""
     import torch
 
     _setenv(monkeypatch, "ISAL_HIP_ENC_XOR", xor)
+    _setenv(monkeypatch, "ISAL_HIP_ENC_LDS", lds)
     if gen == "rs":
         coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
     else:
@@ -702,6 +704,66 @@ def test_pinned_host_shards_read_in_place(engine, oracle, gpu, monkeypatch, capf
     assert oracle.raid("pq_gen", 6, n - 40, vec) == 0
     vec[3][12345] ^= 0x11
     assert pc(6, n - 40, _vp(vec)) == oracle.raid("pq_check", 6, n - 40, [x.copy() for x in vec])
+
+
+def test_partly_registered_host_shard_is_staged(engine, oracle, gpu, monkeypatch, capfd):
+    """A shard whose first bytes lie in a hipHostRegister'ed range but whose
+    tail runs past it must not be read in place (the kernel would touch
+    unmapped memory): the engine checks the shard's last byte and stages it.
+    Shards wholly inside the registration are still used in place."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", "auto")
+    _setenv(monkeypatch, "ISAL_HIP_LOG", "1")
+    _setenv(monkeypatch, "ISAL_HIP_CPU_MAX_BYTES", "0")  # every host call to the GPU
+    page, k, rows, n = 4096, 4, 2, 1 << 20
+    raw = np.zeros((k + rows) * n + 2 * page, np.uint8)
+    off = (-raw.ctypes.data) % page
+    buf = raw[off:off + (k + rows) * n]
+    shard = [buf[i * n:(i + 1) * n] for i in range(k + rows)]
+    for j in range(k):
+        shard[j][:] = fill_bytes(n, 900 + j)
+    coef = fill_bytes(k * rows, 901)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    want = oracle.encode(coef, k, rows, shard[:k])
+    cudart = torch.cuda.cudart()
+    for reg in ((k + rows) * n - n // 2, (k + rows) * n):  # last shard half registered, all registered
+        assert int(cudart.cudaHostRegister(buf.ctypes.data, reg, 0)) == 0
+        try:
+            for l in range(rows):
+                shard[k + l][:] = 0x5A
+            capfd.readouterr()
+            engine.ec_encode_data(n, k, rows, tbls, shard[:k], shard[k:])
+            err = capfd.readouterr().err
+            for l in range(rows):
+                assert np.array_equal(shard[k + l], want[l]), (reg, l)
+            # partly registered: the tail shard is staged; wholly registered: in place
+            assert ("gpu direct" in err) == (reg == (k + rows) * n), err
+        finally:
+            assert int(cudart.cudaHostUnregister(buf.ctypes.data)) == 0
+
+
+def test_copy_helper_cap(engine, oracle, gpu, monkeypatch):
+    """ISAL_HIP_MAX_HELPERS caps the per-thread copy-out helpers of large staged
+    host calls: past the cap a thread issues its copies alone. Results ==
+    oracle with no helper at all and with one helper shared by three threads'
+    worth of calls."""
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", "auto")
+    k, rows, n = 6, 5, (9 << 20) + 48  # pageable, several 4 MiB chunks: the pipelined route
+    coef = fill_bytes(k * rows, 4242)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    src = [fill_bytes(n, 4300 + j) for j in range(k)]
+    want = oracle.encode(coef, k, rows, src)
+    for cap in ("0", "1"):
+        _setenv(monkeypatch, "ISAL_HIP_MAX_HELPERS", cap)
+        outs = [[np.zeros(n, np.uint8) for _ in range(rows)] for _ in range(3)]
+        ths = [threading.Thread(target=engine.ec_encode_data, args=(n, k, rows, tbls, src, outs[t]))
+               for t in range(3)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        for t in range(3):
+            for l in range(rows):
+                assert np.array_equal(outs[t][l], want[l]), (cap, t, l)
 
 
 def test_pinned_calls_take_the_gpu_earlier(engine, oracle, gpu, monkeypatch, capfd):
@@ -1682,6 +1744,37 @@ def test_bench_two_ranks_on_one_gpu(gpu):
     assert out["scaling"] == "strong" and out["value"] > 0
 
 
+def test_c5_full_workload_eight_ranks(gpu):
+    """BASELINE configs[4] (C5) at its real size: 1,048,576 stripes of k=10
+    m=4 1 MiB shards split over 8 ranks — the driver's `bench.py --gpus 8`
+    form with gloo so all eight share this box's one GPU (RCCL needs a GPU
+    per rank; the 8-GPU node runs the same code over it). Every rank encodes
+    its contiguous 131,072-stripe range from resident 256-stripe batches and
+    self-checks three stripes with a decode round trip through every parity
+    row; every stripe-encode is counted."""
+    import json
+    import sys
+
+    env = {a: b for a, b in os.environ.items() if a not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    T, W, steps = 1 << 20, 8, 1
+    r = subprocess.run([sys.executable, os.path.join(ecutil.REPO, "bench.py"), "--gpus", str(W),
+                        "--dist-backend", "gloo", "--total-stripes", str(T), "--len", str(1 << 20),
+                        "--stripes", "256", "--steps", str(steps), "--warmup", "1"],
+                       capture_output=True, text=True, timeout=900, cwd=ecutil.REPO, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    print(json.dumps({a: out[a] for a in ("value", "ms_per_step", "n_gpus", "stripes_encoded", "self_check")}))
+    assert out["n_gpus"] == W and out["scaling"] == "strong"
+    assert out["config"]["stripe_ranges"] == [[q * (T // W), (q + 1) * (T // W)] for q in range(W)], out
+    assert out["config"]["total_stripes"] == T and out["config"]["batch_stripes"] == 256
+    assert out["stripes_encoded"] == T * steps == out["stripes_expected"], out
+    assert out["self_check"] is True and "decode round trip" in out["self_check_method"], out
+    assert out["value"] > 0 and out["shard_crc32c_digest"] > 0
+
+
+FUZZ_RSS_LIMIT_MB = 2048
+
+
 def test_differential_fuzz_on_the_kernels(gpu, tmp_path):
     """tests/fuzz/ec_diff_fuzz.c against the shipped libisal_hip.so with every
     call forced onto the kernels: encode / update / dot / mad / mul / RAID
@@ -1697,13 +1790,18 @@ def test_differential_fuzz_on_the_kernels(gpu, tmp_path):
     subprocess.run([sys.executable, os.path.join(ecutil.REPO, "tests", "fuzz", "seeds.py"), "diff", str(corpus)],
                    check=True, capture_output=True)
     env = dict(os.environ, ISAL_HIP_BACKEND="gpu")
-    r = subprocess.run([exe, "-max_total_time=45", "-max_len=300000", "-print_final_stats=1", "-rss_limit_mb=0",
+    # libFuzzer's own memory bounds, explicit: the process's RSS (HIP runtime
+    # and code objects included) and any single malloc stay under 2 GiB
+    r = subprocess.run([exe, "-max_total_time=45", "-max_len=300000", "-print_final_stats=1",
+                        f"-rss_limit_mb={FUZZ_RSS_LIMIT_MB}", f"-malloc_limit_mb={FUZZ_RSS_LIMIT_MB}",
                         f"-artifact_prefix={tmp_path}/", str(corpus)],
                        capture_output=True, text=True, timeout=240, env=env, cwd=tmp_path)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
-    runs = [int(l.split(":")[-1]) for l in out.splitlines() if l.startswith("stat::number_of_executed_units")]
-    assert runs and runs[0] >= 200, out[-2000:]
+    stat = {l.split(":")[-2]: int(l.split(":")[-1]) for l in out.splitlines()
+            if l.startswith("stat::") and l.split(":")[-1].strip().isdigit()}
+    assert stat.get("number_of_executed_units", 0) >= 200, out[-2000:]
+    assert 0 < stat["peak_rss_mb"] < FUZZ_RSS_LIMIT_MB, stat
 
 
 def test_bench_refuses_more_rccl_ranks_than_gpus(gpu):

@@ -189,12 +189,42 @@ for s in $STEPS; do
                         done
                 done
                 ;;
+        lds)
+                # encode low table halves from LDS (ISAL_HIP_ENC_LDS): parity tests, then A/B per shape
+                run pytest_gpu_lds 600 python -u -m pytest tests -m gpu -x -v -k "xor_fast_path or config_c2 or random_shapes or raid or maximum_stripe or decode" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for shape in ${XOR_SHAPES:-10_4_1048576_1024 20_6_4194304_64 10_8_1048576_1024 10_6_1048576_1024}; do
+                                set -- ${shape//_/ }
+                                for x in 0 1; do
+                                        ISAL_HIP_ENC_LDS=$x run bench_k$1p$2_lds${x}_r$r 300 python bench.py --workload encode --k $1 --p $2 --len $3 --stripes $4 --no-cpu-baseline
+                                done
+                        done
+                done
+                run bench_decode 300 python bench.py --workload decode --no-cpu-baseline
+                ISAL_HIP_ENC_LDS=0 run bench_decode_lds0 300 python bench.py --workload decode --no-cpu-baseline
+                ;;
+        fuzzrss)
+                # the GPU differential fuzz target for 150 s with libFuzzer's 2 GiB RSS /
+                # malloc bounds; its status lines log the process RSS over time
+                mkdir -p "$OUT/fuzz_corpus" && python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
+                ISAL_HIP_BACKEND=gpu run fuzz_rss 240 isa-l_amd/build/fuzzgpu/ec_diff_fuzz_gpu -max_total_time=150 -max_len=300000 -print_final_stats=1 -rss_limit_mb=2048 -malloc_limit_mb=2048 -artifact_prefix="$OUT/" "$OUT/fuzz_corpus"
+                grep -E "rss:|stat::" "$OUT/fuzz_rss.log" | tail -40 > "$OUT/fuzz_rss_summary.txt" || true
+                rm -rf "$OUT/fuzz_corpus"
+                ;;
+        c5test)
+                run pytest_gpu_c5 900 python -u -m pytest tests -m gpu -x -v -s -k "c5_full_workload or two_ranks_on_one_gpu" --timeout 800 --timeout-method thread
+                ;;
+        dropintests)
+                run pytest_gpu_dropin 600 python -u -m pytest tests -m gpu -x -v -k "dropin or concurrent or pinned or golden or device or xor_fast_path or smoke or raid" --timeout 300 --timeout-method thread
+                ;;
         dropin)
                 # the synchronous drop-in call on device-resident C2 stripes, 1/4/16 threads
                 for t in 1 4 16; do
                         run dropin_t$t 120 tools/dropin_bench 10 4 1048576 64 $t 3
                 done
                 run dropin_small_t1 120 tools/dropin_bench 10 4 4096 64 1 3
+                run bench_dropin 300 python bench.py --workload dropin
+                ISAL_HIP_KARG=0 run bench_dropin_nokarg 300 python bench.py --workload dropin
                 run dropin_hiptrace 200 rocprofv3 --hip-trace --kernel-trace --stats --output-format csv -d "$OUT/prof_dropin" -o dropin -- tools/dropin_bench 10 4 1048576 64 1 0 400
                 ;;
         tests_crc)
