@@ -242,6 +242,29 @@ def enc_order() -> int:
     return 0 if os.environ.get("ISAL_HIP_ENC_ORDER") == "0" else 2
 
 
+def enc_kernel(rows: int, k: int, coef) -> str:
+    """The vector encode kernel the library launches for one pass of `rows`
+    (<= 8) outputs with coefficient matrix coef (rows x k): its load group
+    (enc_group), work order (enc_order) and variant — bit 0 the XOR path for
+    0/1 rows and columns (isal_hip_enc_masks: row 0 and column 0 hold only
+    0/1, k <= 64; ISAL_HIP_ENC_XOR=0 off), bit 1 low table halves from LDS
+    (ISAL_HIP_ENC_LDS=0 off); both only in the default order-2 policy."""
+    import numpy as np
+
+    c = np.asarray(coef, dtype=np.uint8).reshape(rows, k)
+    order = enc_order()
+    fl = 0
+    if order == 2 and os.environ.get("ISAL_HIP_ENC_STORE") != "1":
+        if (os.environ.get("ISAL_HIP_ENC_XOR") != "0" and k <= 64 and int(c[0].max()) <= 1
+                and int(c[:, 0].max()) <= 1):
+            fl |= 1
+        if os.environ.get("ISAL_HIP_ENC_LDS") != "0":
+            fl |= 2
+    st = 3 if os.environ.get("ISAL_HIP_ENC_STORE") == "1" and order == 2 else 2
+    base = f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, 2, {st}, {order}>"
+    return base + (f", {fl}>" if fl else ">")
+
+
 def enc_group(k: int) -> int:
     """Sources per load group the engine launches with (ec_kernels.hip:enc_group)."""
     return next((u for u in (12, 10, 8, 6, 5, 4) if k >= u and k % u == 0), 4)
@@ -330,7 +353,8 @@ def pmc_traffic(workload, k, p, n, S, kernel):
         return x[4:] if x.startswith("void") else x
 
     name = norm(kernel)
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_*.csv")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*_pmc_*.csv"), recursive=True),
+                       key=os.path.basename, reverse=True):  # newest round first (rNN_ prefix)
         with open(path) as f:
             lines = f.read().splitlines()
         cfg = next((l for l in lines if l.startswith("# config:")), "")
@@ -358,7 +382,8 @@ def kernel_stats(workload, k, p, n, S, kernel):
 
     want = {"workload": workload, "k": str(k), "p": str(p), "len": str(n), "stripes": str(S)}
     name = kernel.replace(" ", "")
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_kernel_steady.csv")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*_kernel_steady.csv"), recursive=True),
+                       key=os.path.basename, reverse=True):
         with open(path) as f:
             rows = [l.rstrip("\n") for l in f]
         cfg = next((l for l in rows if l.startswith("# config:")), "")
@@ -697,7 +722,7 @@ def total_stripes_run(args, d: Dist, a, k, p, n):
                              "with gf_invert_matrix + the engine, == the originals)",
         "roofline": {
             "bound": "hbm",
-            "kernel": f"ec_encode_v16<{p}, EncPol<{enc_group(k)}, 2, 2, {enc_order()}>>",
+            "kernel": enc_kernel(p, k, a[k * k:]),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -855,7 +880,7 @@ def main(argv=None):
                                [int(frag(s, i).data_ptr()) for s in range(S) for i in surv],
                                [int(out[s, i].data_ptr()) for s in range(S) for i in range(rows)])
         bytes_per_launch = (k + rows) * n * S
-        kernel = f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, 2, 2, {enc_order()}>>"
+        kernel = enc_kernel(rows, k, c)
         workload = f"C3 decode: recover data shards {errs} of k={k} p={p} RS, {n} B shards x {S} stripes/GPU"
     else:
         rows = p
@@ -864,7 +889,7 @@ def main(argv=None):
                                [int(out[s, l].data_ptr()) for s in range(S) for l in range(p)])
         if args.workload == "encode":
             bytes_per_launch = (k + p) * n * S
-            kernel = f"ec_encode_v16<{p}, EncPol<{enc_group(k)}, 2, 2, {enc_order()}>>"
+            kernel = enc_kernel(p, k, a[k * k:])
             workload = f"C2 encode: k={k} p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU"
         elif args.workload in ("encode-crc", "crc"):
             # fragment checksums: crc32_iscsi of all k+p shards,

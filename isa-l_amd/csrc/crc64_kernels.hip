@@ -493,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void crc64_combine(
 constexpr unsigned long long kMaxItems = 1ull << 30;
 
 // Tiles per chain step of crc64_shards (ISAL_HIP_CRC64_STEP = 1, 2 or 4).
-// Measured on the C2 shape (profiles/r01_crc64_step_sweep.txt): 2 tiles per
+// Measured on the C2 shape (profiles/r01/r01_crc64_step_sweep.txt): 2 tiles per
 // step with 4 loads in flight is fastest; 4 per step costs occupancy (LDS).
 int chain_step() {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_STEP);
@@ -508,7 +508,7 @@ bool shards_pre() {
 
 // Pipelined lookups in the pre-shifted kernel (ISAL_HIP_CRC64_PRE_PIPE=1; off
 // by default). C2 shape, same box, two runs each
-// (profiles/r03_crc64_prepipe_benches.jsonl, r03_pmc_sq_crc64_prepipe.txt):
+// (profiles/r03/r03_crc64_prepipe_benches.jsonl, r03_pmc_sq_crc64_prepipe.txt):
 // 2.82-2.85 ms unpipelined vs 2.94-2.95 ms pipelined — SQ_WAIT_INST_LDS fell
 // 41 % but the 56 lookup VGPRs in flight cut the occupancy from 7 to 3 waves
 // per SIMD, and the kernel was not bound by its LDS round trips.
@@ -1038,7 +1038,7 @@ int pair_step() {
 // Source chains in registers when the k sources form one load group only with
 // ISAL_HIP_CRC64_SRC_CHAIN=reg: on the C2 shape the register variant (209
 // VGPRs, 2 waves/SIMD) is 5 % slower than LDS chains at 3 waves/SIMD
-// (profiles/r01_encode_crc64_sweep.txt).
+// (profiles/r01/r01_encode_crc64_sweep.txt).
 bool src_chain_reg64() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC64_SRC_CHAIN) == 1;  // "reg"
 }
@@ -1046,12 +1046,12 @@ bool src_chain_reg64() {
 // Slicing-by-8 chunk path in the fused kernel: on by default
 // (ISAL_HIP_CRC64_SLICE=0 selects the field tables). C2 step, LDS chains, two
 // lane groups: 4.58 -> 4.01 ms (VALU 2.40e9 -> 1.83e9 wave-instructions,
-// profiles/r02_fastcrc_*); with register chains (240 VGPRs) it is slower.
+// profiles/r02/r02_fastcrc_*); with register chains (240 VGPRs) it is slower.
 // 0: field tables, 1: byte (slicing) tables, 2: hybrid tables (experiment,
 // instantiated for the C2 load group U = 10 only; other U use byte tables),
 // 3 (the default; byte tables elsewhere): byte tables with the chain steps
 // pipelined into the GF rows, for load group U = 10 and P <= 4 — C2 step
-// 3.386 -> 3.305 ms (profiles/r03_pipe64_benches.jsonl).
+// 3.386 -> 3.305 ms (profiles/r03/r03_pipe64_benches.jsonl).
 int slice64() {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_SLICE);
   return v == 0 ? 0 : v == 1 ? 1 : v == 2 ? 2 : 3;

@@ -383,7 +383,7 @@ constexpr unsigned kMaxCrcItems = 1u << 30;
 
 // Tiles per chain step of crc32c_shards (ISAL_HIP_CRC_STEP = 1 or 4). Unlike
 // CRC64 the CRC32C kernel is not bound by its lookups: step 4 measured 2.90 ms
-// vs 2.87 ms per C2 step (profiles/r01_crc_step_sweep.txt), so 1 by default.
+// vs 2.87 ms per C2 step (profiles/r01/r01_crc_step_sweep.txt), so 1 by default.
 // Pre-shifted chains in the checksum-only kernel (ISAL_HIP_CRC_PRE=0: the
 // chain-step kernel, with ISAL_HIP_CRC_STEP).
 bool crc_pre() {
@@ -714,7 +714,7 @@ int enc_group_crc(int k) {
 // Source chains in registers when the k sources form one load group only with
 // ISAL_HIP_CRC_SRC_CHAIN=reg: the register variant needs 153 VGPRs (3 waves
 // per SIMD) and was 2 % behind LDS chains on the C2 shape already in round 1
-// (profiles/r01_crc_tile_sweep.txt); LDS chains (117 VGPRs, 4 waves) also
+// (profiles/r01/r01_crc_tile_sweep.txt); LDS chains (117 VGPRs, 4 waves) also
 // take the X0 variant.
 bool src_chain_reg() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC_SRC_CHAIN) == 1;  // "reg"
@@ -724,7 +724,7 @@ bool src_chain_reg() {
 // source chains: all four by default (ISAL_HIP_CRC_BYTE_DWORDS=0 selects the
 // field tables). C2 step 3.74 -> 3.48 ms (VALU 2.11e9 -> 1.65e9
 // wave-instructions; the LDS array is then ~76 % busy, half of it bank
-// conflicts: profiles/r02_fastcrc_*).
+// conflicts: profiles/r02/r02_fastcrc_*).
 int crc_byte_dwords() {
   return isal_hip_knob(ISAL_HIP_KNOB_CRC_BYTE_DWORDS) == 0 ? 0 : 4;
 }

@@ -49,10 +49,10 @@ typedef u32x4 __attribute__((address_space(1)))* gstore_t;
 // Memory access modes: 0 plain global, 1 non-temporal global (nt),
 // 2 non-temporal buffer_load/store (wave-uniform descriptor per shard, 32-bit
 // lane offset; measured +1.3 % over mode 1 on the 10-read/4-write stream,
-// profiles/r01_probe_variants_3.txt). `len` bounds the buffer descriptor.
+// profiles/r01/r01_probe_variants_3.txt). `len` bounds the buffer descriptor.
 // 3 = buffer ops with sc1 + nt (gfx950 CPol 0x12): in the memory probe the
 // 10-read/4-write stream with sc1+nt stores ran +0.5-0.9 % over nt stores
-// (profiles/r03_probe_variants.txt); selectable for the encode's stores.
+// (profiles/r03/r03_probe_variants.txt); selectable for the encode's stores.
 enum : int { kPlain = 0, kNT = 1, kBufNT = 2, kBufSC1NT = 3 };
 
 template <int MODE = kPlain>
@@ -96,12 +96,12 @@ __device__ __forceinline__ void store16(uint64_t base, long long off, uint4 v, i
 //   LD/ST  memory access modes of source loads / parity stores (above)
 //   ORDER  0: work item = (stripe, tile) with tile fastest; 1: stripe fastest;
 //          2: XCD-contiguous
-// Measured on MI355X (profiles/r01_probe_variants_*.txt): non-temporal loads
+// Measured on MI355X (profiles/r01/r01_probe_variants_*.txt): non-temporal loads
 // AND stores lift the 10-read/4-write stream from 5.5 to 6.1 TB/s, issuing
 // all of a stripe's source loads at once (U = k) adds ~1 %, buffer ops ~1 %;
 // shard padding does not help. The XCD-contiguous order (2) measured -2.4 %
 // on one round-1/2 box and +1.0-1.3 % on every round-3 box (same-box A/B,
-// profiles/r03_enc_order_benches.jsonl, r03_probe_variants.txt); the library
+// profiles/r03/r03_enc_order_benches.jsonl, r03_probe_variants.txt); the library
 // launches order 2 by default (ec_kernels.hip enc_order) and picks U from k
 // at launch (enc_group).
 template <int UU, int LDM = kBufNT, int STM = kBufNT, int ORD = 0>

@@ -276,7 +276,7 @@ int enc_group(int k) {
 // stripes; the identity order when nitems % 8 != 0); 0 = (stripe, tile) with
 // tile fastest. Same items, same arithmetic. C2, same box, three runs each:
 // 2.401 -> 2.379 ms and 2.464 -> 2.436 ms on two boxes
-// (profiles/r03_enc_order_benches.jsonl; the memory probe: +1.2 %).
+// (profiles/r03/r03_enc_order_benches.jsonl; the memory probe: +1.2 %).
 int enc_order() {
   return isal_hip_knob(ISAL_HIP_KNOB_ENC_ORDER) == 0 ? 0 : 2;
 }

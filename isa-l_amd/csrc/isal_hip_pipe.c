@@ -62,7 +62,7 @@ isal_hip_pipe_create(isal_hip_pipe **out, int len, int k, int rows, const unsign
         /* More than 4 stripes in flight only slows the copies: with H2D and D2H
          * both streaming, 6-8 queued stripes drop H2D from ~49 to 31-35 GB/s
          * (plain torch copies show the same, tools/pcie_probe.py,
-         * profiles/r02_pcie_probe.txt), so extra slots are not allocated. */
+         * profiles/r02/r02_pcie_probe.txt), so extra slots are not allocated. */
         if (depth > ISAL_HIP_PIPE_MAX_DEPTH)
                 depth = ISAL_HIP_PIPE_MAX_DEPTH;
         p = (isal_hip_pipe *) calloc(1, sizeof(*p));

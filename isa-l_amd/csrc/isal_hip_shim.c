@@ -131,7 +131,7 @@ backend(void)
 /* Host calls of at most this many shard bytes ((k + rows) * len) take the CPU
  * route under ISAL_HIP_BACKEND=auto (override: ISAL_HIP_CPU_MAX_BYTES). Below
  * it the ~30 us GPU round trip costs more than the arithmetic (DESIGN.md §3,
- * measured crossover in profiles/r02_route_crossover.txt). */
+ * measured crossover in profiles/r02/r02_route_crossover.txt). */
 #define DEFAULT_CPU_MAX_BYTES ((size_t) 8 << 20)
 
 static size_t
@@ -144,7 +144,7 @@ cpu_max_bytes(void)
 /* The same limit for calls whose host shards are all page-locked and used in
  * place by the kernels (no staging copy): there the GPU wins from 1.8 MB
  * (k = 10, p = 4: 51.6 vs 59.1 us; 14.7 MB: 290 vs 497 us,
- * profiles/r03_route_crossover_c.jsonl). Override: ISAL_HIP_CPU_MAX_BYTES_PINNED
+ * profiles/r03/r03_route_crossover_c.jsonl). Override: ISAL_HIP_CPU_MAX_BYTES_PINNED
  * (ISAL_HIP_CPU_MAX_BYTES also lowers it). */
 #define DEFAULT_CPU_MAX_BYTES_PINNED ((size_t) 2 << 20)
 
@@ -812,7 +812,7 @@ job_add(copyjob_t *j, void *dst, const void *src, size_t bytes, hipMemcpyKind ki
  * calling thread's worker (ISAL_HIP_PAR_COPY=0: not): a pageable copy runs
  * synchronously on the thread that issues it with a fixed cost of ~14 us,
  * and a second issuing thread hides part of it (H2D of 2 MiB shards:
- * 36 -> 41 GB/s, profiles/r03_stage_probe_b.jsonl). The worker copies in on
+ * 36 -> 41 GB/s, profiles/r03/r03_stage_probe_b.jsonl). The worker copies in on
  * s_out (the kernel waits for its event); for an encode it also copies half
  * the parity out after the kernel. An update's parity comes back from this
  * thread alone, in row order, so a failure leaves a known prefix of rows
@@ -995,9 +995,9 @@ gpu_chunked(ctx_t *c, int op, int len, int k, int rows, int vec_i, const unsigne
 /* Column-chunk bytes per shard of a pipelined call: ISAL_HIP_CHUNK_KB, else
  * DEFAULT_CHUNK_BYTES. Every chunk costs one copy per staged shard each way,
  * and a copy from or to pageable memory has a fixed cost of ~14 us beside its
- * bytes (profiles/r03_calltrace.txt), so chunks must be large: at 16 MiB
+ * bytes (profiles/r03/r03_calltrace.txt), so chunks must be large: at 16 MiB
  * shards 4 MiB chunks beat one chunk by 4-9 %, 1 MiB chunks lose 50 %
- * (profiles/r03_chunk_sweep*.jsonl). */
+ * (profiles/r03/r03_chunk_sweep*.jsonl). */
 static size_t
 chunk_bytes(void)
 {
@@ -1795,7 +1795,7 @@ isal_hip_batch_destroy(isal_hip_batch *b)
 
 /* Tiles per CRC workgroup: `def` (64 for both CRC32C and CRC64: 256 KiB of
  * each shard per block, partials 0.1 % (CRC32C) / 0.2 % (CRC64) of the bytes
- * — profiles/r02_crc_tiles_sweep_b.jsonl, r03_crc_tiles_sweep.jsonl), halved
+ * — profiles/r02/r02_crc_tiles_sweep_b.jsonl, r03_crc_tiles_sweep.jsonl), halved
  * while the launch would have fewer than 2048 workgroups.
  * ISAL_HIP_CRC_TILES overrides. */
 static int
@@ -1826,7 +1826,7 @@ batch_crc_setup(isal_hip_batch *b)
                 return ISAL_HIP_OK;
         /* 64 tiles per block: the checksum-only pass is memory-side bound and runs
          * 12 % faster than at 16, the fused pass is flat from 16 to 64
-         * (profiles/r02_crc_tiles_sweep_b.jsonl) */
+         * (profiles/r02/r02_crc_tiles_sweep_b.jsonl) */
         isal_hip_crc_geometry(b->len, crc_tiles(b->len, b->nstripes, 64), &b->crc);
         nsh = (size_t) b->nstripes * (size_t) (b->k + b->rows);
         part = nsh * (size_t) b->crc.nblk * 256;
@@ -1908,7 +1908,7 @@ batch_crc64_setup(isal_hip_batch *b, int variant)
         if (!b->d_c64part && !b->c64_tt) {
                 /* 64 tiles per block: the checksum-only pass runs 2.7 % faster
                  * than at 32, the fused pass is flat from 32 to 64
-                 * (profiles/r03_crc_tiles_sweep.jsonl) */
+                 * (profiles/r03/r03_crc_tiles_sweep.jsonl) */
                 b->c64_tt = crc_tiles(b->len, b->nstripes, 64);
                 isal_hip_crc64_geometry(b->len, b->c64_tt, &g);
                 if (g.nblk) {

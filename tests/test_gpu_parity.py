@@ -1470,7 +1470,7 @@ CONFORMANCE = ["gf_inverse_test", "gf_vect_mul_test", "gf_vect_mul_base_test",
 # xor_check_test / pq_check_test sweep every (length, error position, vector)
 # with ~1.6e7 small synchronous calls each: at a ~30 us GPU round trip per call
 # that is ~10 minutes apiece, so under ISAL_HIP_BACKEND=gpu they run only with
-# ISAL_SLOW_CONFORMANCE=1 (logs: profiles/r01_slow_conformance_*.log). Under
+# ISAL_SLOW_CONFORMANCE=1 (logs: profiles/r01/r01_slow_conformance_*.log). Under
 # the library's default routing (auto: small host calls on the CPU route, the
 # rest on the GPU) all thirteen run.
 SLOW_CONFORMANCE = {"xor_check_test", "pq_check_test"}

@@ -170,7 +170,29 @@ for s in $STEPS; do
                 run bench_c2 300 python bench.py --no-cpu-baseline
                 cp "$OUT/bench_c2.log" "$OUT/bench_c2.json"
                 run rocprof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c2" -o c2 -- python3 bench.py --no-cpu-baseline
-                run steady_c2 60 python3 tools/kernel_stats.py "$OUT/prof_c2" ec_encode_v16 --skip 5 --keep 20 --bytes 15032385536 --out "$OUT/c2_encode_kernel_steady.csv" --config "workload=encode k=10 p=4 len=1048576 stripes=1024" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline"
+                run steady_c2 60 python3 tools/kernel_stats.py "$OUT/prof_c2" "ec_encode_v16<4" --skip 5 --keep 20 --bytes 15032385536 --out "$OUT/c2_encode_kernel_steady.csv" --config "workload=encode k=10 p=4 len=1048576 stripes=1024" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline"
+                ;;
+        headline)
+                # the round's headline evidence for one tree: C2 line (with the CPU
+                # baseline), its rocprofv3 trace + steady-state summary, PMC traffic;
+                # C3 decode the same way
+                run bench_c2 300 python bench.py
+                cp "$OUT/bench_c2.log" "$OUT/bench_c2.json"
+                run rocprof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c2" -o c2 -- python3 bench.py --no-cpu-baseline
+                run steady_c2 60 python3 tools/kernel_stats.py "$OUT/prof_c2" "ec_encode_v16<4" --skip 5 --keep 20 --bytes 15032385536 --out "$OUT/c2_encode_kernel_steady.csv" --config "workload=encode k=10 p=4 len=1048576 stripes=1024" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline"
+                run pmc_fetch_c2 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c2" -o f -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1
+                run pmc_write_c2 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c2" -o w -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1
+                python3 tools/pmc_csv.py "$OUT/pmc_c2_encode.csv" "workload=encode k=10 p=4 len=1048576 stripes=1024" "python bench.py --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_c2" "$OUT/pmc_write_c2" ec_encode_v16
+                run pmc_sq_c2 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_c2" -o s -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1
+                run bench_decode 300 python bench.py --workload decode --cpu-seconds 5
+                cp "$OUT/bench_decode.log" "$OUT/bench_decode.json"
+                run rocprof_decode 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_decode" -o decode -- python3 bench.py --workload decode --no-cpu-baseline
+                run steady_decode 60 python3 tools/kernel_stats.py "$OUT/prof_decode" "ec_encode_v16<3" --skip 5 --keep 20 --bytes 13958643712 --out "$OUT/decode_encode_kernel_steady.csv" --config "workload=decode k=10 p=4 len=1048576 stripes=1024" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --workload decode --no-cpu-baseline"
+                run pmc_fetch_decode 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_decode" -o f -- python3 bench.py --workload decode --no-cpu-baseline --steps 3 --warmup 1
+                run pmc_write_decode 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_decode" -o w -- python3 bench.py --workload decode --no-cpu-baseline --steps 3 --warmup 1
+                python3 tools/pmc_csv.py "$OUT/pmc_decode.csv" "workload=decode k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload decode --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_decode" "$OUT/pmc_write_decode" ec_encode_v16
+                run bench_c2_final 300 python bench.py --no-cpu-baseline
+                cp "$OUT/bench_c2_final.log" "$OUT/bench_c2_final.json"
                 ;;
         wide)
                 # wide-stripe encode: device-resident shapes beyond C2's p = 4
