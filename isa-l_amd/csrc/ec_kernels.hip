@@ -201,10 +201,9 @@ __device__ __forceinline__ void mad_bytes(const uint64_t* __restrict__ sp, int s
 }
 
 template <int P>
-__global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restrict__ ptrs,
-                                                        int ptr_stride, int src_idx, int dst0,
-                                                        const uint32_t* __restrict__ tbl, int len,
-                                                        unsigned nitems, unsigned tiles, int xcd) {
+__device__ __forceinline__ void update_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src_idx,
+                                             int dst0, const uint32_t* __restrict__ tbl, int len,
+                                             unsigned nitems, unsigned tiles, int xcd) {
   for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
     const unsigned w = xcd_item(ww, nitems, xcd);
     const unsigned stripe = w / tiles;
@@ -230,6 +229,22 @@ __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restri
       mad_bytes<P>(sp, src_idx, dst0, tbl, off, static_cast<int>(len - off));
     }
   }
+}
+
+template <int P>
+__global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restrict__ ptrs,
+                                                        int ptr_stride, int src_idx, int dst0,
+                                                        const uint32_t* __restrict__ tbl, int len,
+                                                        unsigned nitems, unsigned tiles, int xcd) {
+  update_items<P>(ptrs, ptr_stride, src_idx, dst0, tbl, len, nitems, tiles, xcd);
+}
+
+// One update call whose pointers (source, then P parity rows) and the source's
+// P coefficient tables travel as kernel arguments (as ec_encode_karg).
+template <int P>
+__global__ __launch_bounds__(kBlock) void ec_update_karg(const isal_hip_karg a, int len, unsigned tiles) {
+  const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
+  update_items<P>(ka->ptrs, 1 + P, 0, 1, ka->tbl, len, tiles, tiles, 0);
 }
 
 template <int P>
@@ -435,6 +450,23 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int 
 #undef EC_KARG_U
 #undef EC_KARG
     default: return static_cast<int>(hipErrorInvalidValue);
+  }
+  isal_hip_count_launch();
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int isal_hip_launch_update_karg(const isal_hip_karg* a, int len, int rows, void* stream) {
+  if (len <= 0 || rows <= 0) return 0;
+  if (rows > EC_MAX_ROWS_PER_PASS) return static_cast<int>(hipErrorInvalidValue);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + kTile - 1) / kTile);
+  switch (rows) {
+#define EC_UKARG(n)                                                                                   \
+  case n:                                                                                             \
+    hipLaunchKernelGGL(ec_update_karg<n>, dim3(tiles), dim3(kBlock), 0, s, *a, len, tiles);           \
+    break;
+    EC_UKARG(1) EC_UKARG(2) EC_UKARG(3) EC_UKARG(4) EC_UKARG(5) EC_UKARG(6) EC_UKARG(7) EC_UKARG(8)
+#undef EC_UKARG
   }
   isal_hip_count_launch();
   return static_cast<int>(hipGetLastError());

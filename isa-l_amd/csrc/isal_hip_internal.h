@@ -74,6 +74,9 @@ typedef struct {
 } isal_hip_karg;
 int isal_hip_launch_encode_karg(const isal_hip_karg *a, int len, int k, int rows,
                                 const isal_hip_encmask *em, void *stream);
+/* ec_encode_data_update of one stripe the same way: ptrs = {source, rows
+ * parity}, tbl = the source's tables for rows <= EC_MAX_ROWS_PER_PASS outputs. */
+int isal_hip_launch_update_karg(const isal_hip_karg *a, int len, int rows, void *stream);
 int isal_hip_launch_update(const uint64_t *d_ptrs, int ptr_stride, int src_idx, int dst_idx0,
                            const uint32_t *d_tbl, int len, int k, int rows, int vec_i,
                            long long nstripes, int vec16, void *stream);

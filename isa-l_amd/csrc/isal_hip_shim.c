@@ -1375,11 +1375,12 @@ quiesce(ctx_t *c)
  * argument upload — for device-resident, 16-byte aligned shards of a
  * one-pass stripe that fits the 2 KiB argument block. */
 static int
-karg_fits(int len, int k, int rows, const uint64_t *view, int nptr)
+karg_fits(int op, int len, int k, int rows, const uint64_t *view, int nptr)
 {
         int i;
         if (len < 16 || rows > EC_MAX_ROWS_PER_PASS || nptr > ISAL_HIP_KARG_PTRS ||
-            isal_hip_tables_dwords(k, rows) > ISAL_HIP_KARG_TBL || isal_hip_knob(ISAL_HIP_KNOB_KARG) == 0)
+            isal_hip_tables_dwords(op == OP_UPDATE ? 1 : k, rows) > ISAL_HIP_KARG_TBL ||
+            isal_hip_knob(ISAL_HIP_KNOB_KARG) == 0)
                 return 0;
         for (i = 0; i < nptr; i++)
                 if (view[i] & 15)
@@ -1388,13 +1389,22 @@ karg_fits(int len, int k, int rows, const uint64_t *view, int nptr)
 }
 
 static gpu_res
-gpu_karg(ctx_t *c, int len, int k, int rows, const uint64_t *view, const uint32_t *tbl,
+gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *view, const uint32_t *tbl,
          const isal_hip_encmask *em)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
+        const int nsrc = op == OP_UPDATE ? 1 : k;
         isal_hip_karg a;
         memset(&a, 0, sizeof(a));
-        memcpy(a.ptrs, view, sizeof(uint64_t) * (size_t) (k + rows));
+        memcpy(a.ptrs, view, sizeof(uint64_t) * (size_t) (nsrc + rows));
+        if (op == OP_UPDATE) {
+                /* one pass: source vec_i's tables for every row are contiguous */
+                memcpy(a.tbl, tbl + isal_hip_tables_dwords(vec_i, rows), isal_hip_tables_dwords(1, rows) * 4);
+                GPU_TRY_AT(r, FAULT_LAUNCH, (hipError_t) isal_hip_launch_update_karg(&a, len, rows, c->stream));
+                GPU_TRY_AT(r, FAULT_SYNC, hipStreamSynchronize(c->stream));
+                r.done = len;
+                return r;
+        }
         memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
         GPU_TRY_AT(r, FAULT_LAUNCH, (hipError_t) isal_hip_launch_encode_karg(&a, len, k, rows, em, c->stream));
         GPU_TRY_AT(r, FAULT_SYNC, hipStreamSynchronize(c->stream));
@@ -1507,9 +1517,9 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         if (!c) {
                 r.done = 0;
                 r.first_bad = ~0ull;
-        } else if (ndev == nptr && op == OP_ENCODE && karg_fits(len, k, rows, view, nptr)) {
+        } else if (ndev == nptr && op != OP_VERIFY && karg_fits(op, len, k, rows, view, nptr)) {
                 route_log(op, len, k, rows, "gpu kernel-args", "device shards");
-                r = gpu_karg(c, len, k, rows, view, tbl, em);
+                r = gpu_karg(c, op, len, k, rows, vec_i, view, tbl, em);
         } else if (bytes <= ZC_BYTES || (nstage && (size_t) len * (size_t) nstage <= PACK_BYTES)) {
                 const int zc = bytes <= ZC_BYTES;
                 route_log(op, len, k, rows, zc ? "gpu zero-copy" : "gpu packed",
