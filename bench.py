@@ -248,7 +248,8 @@ def enc_kernel(rows: int, k: int, coef) -> str:
     (enc_group), work order (enc_order) and variant — bit 0 the XOR path for
     0/1 rows and columns (isal_hip_enc_masks: row 0 and column 0 hold only
     0/1, k <= 64; ISAL_HIP_ENC_XOR=0 off), bit 1 low table halves from LDS
-    (ISAL_HIP_ENC_LDS=0 off); both only in the default order-2 policy."""
+    (5-6 looked-up rows; ISAL_HIP_ENC_LDS=1 always, =0 never); both only in
+    the default order-2 policy."""
     import numpy as np
 
     c = np.asarray(coef, dtype=np.uint8).reshape(rows, k)
@@ -258,7 +259,8 @@ def enc_kernel(rows: int, k: int, coef) -> str:
         if (os.environ.get("ISAL_HIP_ENC_XOR") != "0" and k <= 64 and int(c[0].max()) <= 1
                 and int(c[:, 0].max()) <= 1):
             fl |= 1
-        if os.environ.get("ISAL_HIP_ENC_LDS") != "0":
+        lds = os.environ.get("ISAL_HIP_ENC_LDS")
+        if lds == "1" or (lds != "0" and rows - (fl & 1) > 4 and rows <= 6):  # ec_kernels.hip enc_lds
             fl |= 2
     st = 3 if os.environ.get("ISAL_HIP_ENC_STORE") == "1" and order == 2 else 2
     base = f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, 2, {st}, {order}>"

@@ -302,9 +302,17 @@ bool enc_store_sc1() {
   return isal_hip_knob(ISAL_HIP_KNOB_ENC_STORE) == 1;
 }
 
-// Low table halves from LDS (kEncLds; ISAL_HIP_ENC_LDS=0: from SGPRs).
-bool enc_lds() {
-  return isal_hip_knob(ISAL_HIP_KNOB_ENC_LDS) != 0;
+// Low table halves from LDS (kEncLds). Same-box A/B, two runs each
+// (profiles/r04_lds_ab.jsonl, with the XOR path): k20p6 0.635 -> 0.663 of
+// 8 TB/s, k10p6 0.752 -> 0.754, C2 0.7705 -> 0.7695, k10p8 0.715 -> 0.702,
+// decode (p = 3) 0.742 -> 0.744. It pays where pairing from SGPRs is not
+// possible (more than 4 looked-up rows) and the pass is not so wide that 3
+// waves per SIMD starve it: 5-6 rows. ISAL_HIP_ENC_LDS=1 forces it for every
+// width, =0 turns it off.
+bool enc_lds(int P, bool x) {
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_LDS);
+  if (v == 0 || v == 1) return v == 1;
+  return P - (x ? 1 : 0) > 4 && P <= 6;
 }
 
 template <int P>
@@ -321,11 +329,11 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
   if (enc_order() == 2 && enc_store_sc1())
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufSC1NT, 2>>), dim3(grid), dim3(kBlock), 0, s,
                        ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
-  else if (enc_order() == 2 && enc_lds() && x)
+  else if (enc_order() == 2 && enc_lds(P, x) && x)
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncXor | kEncLds>), dim3(grid),
                        dim3(kBlock), lds_bytes<P>(k), s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems,
                        tiles, r0m, c0m);
-  else if (enc_order() == 2 && enc_lds())
+  else if (enc_order() == 2 && enc_lds(P, x))
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncLds>), dim3(grid), dim3(kBlock),
                        lds_bytes<P>(k), s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
   else if (enc_order() == 2 && x)

@@ -155,9 +155,10 @@ enum {
         ISAL_HIP_KNOB_ENC_STORE,       /* vector encode stores: 1 sc1 + nt (A/B) | nt */
         ISAL_HIP_KNOB_CRC64_PRE_PIPE,  /* checksum-only CRC64: 1 pipelined lookups (slower; off) */
         ISAL_HIP_KNOB_ENC_XOR,         /* 0: the encode computes 0/1 rows and columns with lookups too */
-        ISAL_HIP_KNOB_ENC_LDS,         /* 0: the encode's low table halves from SGPRs (v_mov), not LDS */
+        ISAL_HIP_KNOB_ENC_LDS,         /* encode low table halves from LDS: 1 always, 0 never (default: 5-6 looked-up rows) */
         ISAL_HIP_KNOB_KARG,            /* 0: device-resident drop-in encodes upload their arguments */
         ISAL_HIP_KNOB_MAX_HELPERS,     /* copy-out helper threads per process (default 8) */
+        ISAL_HIP_KNOB_SYNC_SPIN,       /* 1: synchronous calls poll hipStreamQuery instead of blocking (A/B) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

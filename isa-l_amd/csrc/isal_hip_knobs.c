@@ -59,6 +59,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_ENC_LDS] = {"ISAL_HIP_ENC_LDS", NULL},
         [ISAL_HIP_KNOB_KARG] = {"ISAL_HIP_KARG", NULL},
         [ISAL_HIP_KNOB_MAX_HELPERS] = {"ISAL_HIP_MAX_HELPERS", NULL},
+        [ISAL_HIP_KNOB_SYNC_SPIN] = {"ISAL_HIP_SYNC_SPIN", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];

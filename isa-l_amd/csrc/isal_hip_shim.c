@@ -1388,6 +1388,21 @@ karg_fits(int op, int len, int k, int rows, const uint64_t *view, int nptr)
         return 1;
 }
 
+/* The end of a kernel-argument call: hipStreamSynchronize, or with
+ * ISAL_HIP_SYNC_SPIN=1 a poll of hipStreamQuery (an A/B of the wake-up
+ * latency; the call trace shows ~9 us between the kernel's end and the
+ * synchronisation returning, profiles/r04_dropin_hiptrace_b.txt). */
+static hipError_t
+sync_call(hipStream_t s)
+{
+        hipError_t e;
+        if (isal_hip_knob(ISAL_HIP_KNOB_SYNC_SPIN) != 1)
+                return hipStreamSynchronize(s);
+        while ((e = hipStreamQuery(s)) == hipErrorNotReady)
+                __builtin_ia32_pause();
+        return e;
+}
+
 static gpu_res
 gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *view, const uint32_t *tbl,
          const isal_hip_encmask *em)
@@ -1401,13 +1416,13 @@ gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *
                 /* one pass: source vec_i's tables for every row are contiguous */
                 memcpy(a.tbl, tbl + isal_hip_tables_dwords(vec_i, rows), isal_hip_tables_dwords(1, rows) * 4);
                 GPU_TRY_AT(r, FAULT_LAUNCH, (hipError_t) isal_hip_launch_update_karg(&a, len, rows, c->stream));
-                GPU_TRY_AT(r, FAULT_SYNC, hipStreamSynchronize(c->stream));
+                GPU_TRY_AT(r, FAULT_SYNC, sync_call(c->stream));
                 r.done = len;
                 return r;
         }
         memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
         GPU_TRY_AT(r, FAULT_LAUNCH, (hipError_t) isal_hip_launch_encode_karg(&a, len, k, rows, em, c->stream));
-        GPU_TRY_AT(r, FAULT_SYNC, hipStreamSynchronize(c->stream));
+        GPU_TRY_AT(r, FAULT_SYNC, sync_call(c->stream));
         r.done = len;
         return r;
 }

@@ -248,6 +248,19 @@ for s in $STEPS; do
         c5test)
                 run pytest_gpu_c5 900 python -u -m pytest tests -m gpu -x -v -s -k "c5_full_workload or two_ranks_on_one_gpu" --timeout 800 --timeout-method thread
                 ;;
+        sqwide)
+                # SQ counters of the wide encodes with and without LDS table halves
+                for shape in ${SQ_SHAPES:-20_6_4194304_64 10_8_1048576_1024}; do
+                        set -- ${shape//_/ }
+                        for x in 0 1; do
+                                ISAL_HIP_ENC_LDS=$x run pmc_sq_k$1p$2_lds$x 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_k$1p$2_lds$x" -o s -- python3 bench.py --workload encode --k $1 --p $2 --len $3 --stripes $4 --no-cpu-baseline --steps 2 --warmup 1
+                        done
+                done
+                ;;
+        dropinspin)
+                run bench_dropin_block 300 python bench.py --workload dropin
+                ISAL_HIP_SYNC_SPIN=1 run bench_dropin_spin 300 python bench.py --workload dropin
+                ;;
         dropintests)
                 run pytest_gpu_dropin 600 python -u -m pytest tests -m gpu -x -v -k "dropin or concurrent or pinned or golden or device or xor_fast_path or smoke or raid" --timeout 300 --timeout-method thread
                 ;;
