@@ -960,9 +960,6 @@ def main(argv=None):
             if os.environ.get("ISAL_HIP_CRC_PRE") == "0":
                 m = {"1": 1, "4": 4}.get(os.environ.get("ISAL_HIP_CRC64_STEP", ""), 2)
                 kernel = f"crc64_shards<true, {m}, {b8}>"
-            elif os.environ.get("ISAL_HIP_CRC64_PRE_PIPE") == "2":  # two items per lane
-                b2 = 2 if os.environ.get("ISAL_HIP_CRC64_BATCH") == "2" else b8
-                kernel = f"crc64_shards_pre2<{b2}>"
             else:
                 pp = str(os.environ.get("ISAL_HIP_CRC64_PRE_PIPE") == "1").lower()
                 kernel = f"crc64_shards_pre<{b8}, {pp}>"

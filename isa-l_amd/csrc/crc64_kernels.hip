@@ -343,83 +343,6 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
   }
 }
 
-// Two items per lane (ISAL_HIP_CRC64_PRE_PIPE=2, an A/B variant): a workgroup
-// runs items 2q and 2q + 1 side by side, so every lane carries two independent
-// chains and each chain step has the other chain's lookups to overlap with,
-// without the lookup registers of the pipelined form. Same tables, same
-// partials layout (crc64_combine is unchanged).
-template <int B>
-__global__ __launch_bounds__(kBlock) void crc64_shards_pre2(const uint64_t* __restrict__ ptrs,
-                                                            int ptr_stride, int nsh, int len,
-                                                            unsigned nitems, unsigned nblk,
-                                                            unsigned tt, unsigned nfull, int uswap,
-                                                            const uint64_t* __restrict__ tabs,
-                                                            uint64_t* __restrict__ part) {
-  __shared__ uint64_t lt[2 * kCE];  // F_u, F'_u
-  load_lds<2 * kCE>(lt, tabs + ISAL_HIP_CRC64_PRE_TAB);
-  __syncthreads();
-  const long long lane = threadIdx.x * kVec;
-  auto step = [&](unsigned t, unsigned t1, X64 b, const uint4& x) __attribute__((always_inline)) {
-    X64 c{0u, 0u};
-    if (t + 1 == t1)
-      chunk_acc(c, lt, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
-    else
-      chunk_acc(c, lt + kCE, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
-    return c;
-  };
-  auto geom = [&](unsigned w, uint64_t& base, unsigned& t0, unsigned& t1) __attribute__((always_inline)) {
-    const unsigned si = w / nblk, blk = w - si * nblk;
-    const unsigned stripe = si / nsh, i = si - stripe * nsh;
-    base = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
-    t0 = blk * tt;
-    t1 = t0 + tt < nfull ? t0 + tt : nfull;
-  };
-  const unsigned npair = (nitems + 1) / 2;
-  for (unsigned q = blockIdx.x; q < npair; q += gridDim.x) {
-    const unsigned w0 = 2 * q, w1 = w0 + 1;
-    uint64_t base0, base1 = 0;
-    unsigned ta, t1a, tb = 0, t1b = 0;
-    geom(w0, base0, ta, t1a);
-    if (w1 < nitems) geom(w1, base1, tb, t1b);
-    X64 a{0u, 0u}, b{0u, 0u};
-    // both chains, B tiles each per batch, the next batches' loads in flight
-    uint4 xa[B], xb[B];
-    if (ta + B <= t1a && tb + B <= t1b) {
-#pragma unroll
-      for (int g = 0; g < B; ++g) {
-        xa[g] = load16<kBufNT>(base0, static_cast<long long>(ta + g) * kTile + lane, len);
-        xb[g] = load16<kBufNT>(base1, static_cast<long long>(tb + g) * kTile + lane, len);
-      }
-    }
-    for (; ta + B <= t1a && tb + B <= t1b; ta += B, tb += B) {
-      uint4 ya[B], yb[B];
-#pragma unroll
-      for (int g = 0; g < B; ++g) {
-        ya[g] = xa[g];
-        yb[g] = xb[g];
-      }
-      if (ta + 2 * B <= t1a && tb + 2 * B <= t1b) {
-#pragma unroll
-        for (int g = 0; g < B; ++g) {
-          xa[g] = load16<kBufNT>(base0, static_cast<long long>(ta + B + g) * kTile + lane, len);
-          xb[g] = load16<kBufNT>(base1, static_cast<long long>(tb + B + g) * kTile + lane, len);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < B; ++g) {
-        a = step(ta + g, t1a, a, ya[g]);
-        b = step(tb + g, t1b, b, yb[g]);
-      }
-    }
-    // what is left of either item, one chain at a time
-    for (; ta < t1a; ++ta) a = step(ta, t1a, a, load16<kBufNT>(base0, static_cast<long long>(ta) * kTile + lane, len));
-    for (; tb < t1b; ++tb) b = step(tb, t1b, b, load16<kBufNT>(base1, static_cast<long long>(tb) * kTile + lane, len));
-    const uint64_t ra = a.get(), rb = b.get();
-    part[static_cast<size_t>(w0) * kBlock + threadIdx.x] = uswap ? __builtin_bswap64(ra) : ra;
-    if (w1 < nitems) part[static_cast<size_t>(w1) * kBlock + threadIdx.x] = uswap ? __builtin_bswap64(rb) : rb;
-  }
-}
-
 // v(L) <- sum over lanes of Z^(16 * (255 - L)) v(L), result in red[0]:
 // 8 levels, level s joins lanes L and L + 2^s with Z^(16 * 2^s).
 __device__ __forceinline__ uint64_t lane_tree(uint64_t* red, const uint64_t* tree) {
@@ -512,10 +435,8 @@ bool shards_pre() {
 // 2.82-2.85 ms unpipelined vs 2.94-2.95 ms pipelined — SQ_WAIT_INST_LDS fell
 // 41 % but the 56 lookup VGPRs in flight cut the occupancy from 7 to 3 waves
 // per SIMD, and the kernel was not bound by its LDS round trips.
-// =2: two items per lane (crc64_shards_pre2).
-int pre_pipe() {
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_PRE_PIPE);
-  return v == 1 || v == 2 ? static_cast<int>(v) : 0;
+bool pre_pipe() {
+  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_PRE_PIPE) == 1;
 }
 
 // Full tiles loaded per batch (ISAL_HIP_CRC64_BATCH = 4 or 8), in the
@@ -1203,15 +1124,8 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
   hipLaunchKernelGGL((crc64_shards_pre<B, PP>), dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, \
                      len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),          \
                      static_cast<unsigned>(g.nfull), !refl, d_tabs, part, xcd_order())
-#define PRE2_LAUNCH(B)                                                                                 \
-  hipLaunchKernelGGL(crc64_shards_pre2<B>, dim3((nitems + 1) / 2), dim3(kBlock), 0, s, ptrs, ptr_stride, \
-                     nsh, len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),     \
-                     static_cast<unsigned>(g.nfull), !refl, d_tabs, part)
-        const int pp = pre_pipe(), b2 = isal_hip_knob(ISAL_HIP_KNOB_CRC64_BATCH) == 2;
-        if (pp == 1) { if (b8) PRE_LAUNCH(8, true); else PRE_LAUNCH(4, true); }
-        else if (pp == 2) { if (b8) PRE2_LAUNCH(8); else if (b2) PRE2_LAUNCH(2); else PRE2_LAUNCH(4); }
+        if (pre_pipe()) { if (b8) PRE_LAUNCH(8, true); else PRE_LAUNCH(4, true); }
         else { if (b8) PRE_LAUNCH(8, false); else PRE_LAUNCH(4, false); }
-#undef PRE2_LAUNCH
 #undef PRE_LAUNCH
       } else if (!vec16)
         SHARDS_LAUNCH(false, 1, 4);

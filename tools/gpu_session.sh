@@ -136,18 +136,6 @@ for s in $STEPS; do
                 # the driver's N>1 form on this one-GPU box: two gloo ranks share the GPU
                 run bench_gpus2_gloo 300 python bench.py --gpus 2 --dist-backend gloo --no-cpu-baseline
                 ;;
-        pre2)
-                # checksum-only CRC64: one item per lane (0) vs two interleaved items per lane (2), batch 2/4
-                run pytest_gpu_pre2 400 python -u -m pytest tests -m gpu -x -v -k "crc64 and not encode" --timeout 200 --timeout-method thread
-                for r in 1 2; do
-                        for cfg in 0:4 2:4 2:2; do
-                                ISAL_HIP_CRC64_PRE_PIPE=${cfg%:*} ISAL_HIP_CRC64_BATCH=${cfg#*:} run bench_crc64_pp${cfg/:/_b}_r$r 300 python bench.py --workload crc64 --no-cpu-baseline
-                        done
-                done
-                for cfg in 2:2 2:4; do
-                        ISAL_HIP_CRC64_PRE_PIPE=${cfg%:*} ISAL_HIP_CRC64_BATCH=${cfg#*:} run pmc_lds_crc64_pp${cfg/:/_b} 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_crc64_pp${cfg/:/_b}" -o l -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 2 --warmup 1
-                done
-                ;;
         encstore)
                 # encode parity stores: nt (0, default) vs sc1 + nt (1), interleaved
                 run pytest_gpu_encstore 300 python -u -m pytest tests -m gpu -x -v -k "xcd_order_vs_oracle" --timeout 200 --timeout-method thread
