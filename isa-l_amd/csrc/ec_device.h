@@ -295,16 +295,20 @@ constexpr int enc_pair() {
 // every row's sum as x & m (acc must be zero), in later groups it is an
 // ordinary lookup — and the pairs are (j+1, j+2), ...: one loop body for
 // both, so the register budget is that of one group.
-template <int P, int U, int MODE = kPlain, int FL = kEncLUT>
-__device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
-                                        int j, long long off, const uint32_t* __restrict__ tbl,
-                                        int len, unsigned long long r0m = 0, unsigned c0m = 0,
-                                        const uint2* lt = nullptr) {
-  constexpr bool X = (FL & kEncXor) != 0;
-  constexpr bool LT = (FL & kEncLds) != 0;
-  uint4 x[U];
+template <int U, int MODE>
+__device__ __forceinline__ void enc_load_group(uint4 (&x)[U], const uint64_t* __restrict__ sp, int j, long long off,
+                                           int len) {
 #pragma unroll
   for (int u = 0; u < U; ++u) x[u] = load16<MODE>(sp[j + u], off, len);
+}
+
+// Fold the already-loaded sources j..j+U-1 into acc (see chunk16).
+template <int P, int U, int FL>
+__device__ __forceinline__ void enc_fold_group(uint32_t (&acc)[P][4], const uint4 (&x)[U], int j,
+                                           const uint32_t* __restrict__ tbl, unsigned long long r0m,
+                                           unsigned c0m, const uint2* lt) {
+  constexpr bool X = (FL & kEncXor) != 0;
+  constexpr bool LT = (FL & kEncLds) != 0;
   constexpr int U0 = X ? 1 : 0;
   if constexpr (X) {
     if (j == 0) {
@@ -337,6 +341,16 @@ __device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* _
                     lt + (j + U - 1) * P);
     __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+template <int P, int U, int MODE = kPlain, int FL = kEncLUT>
+__device__ __forceinline__ void chunk16(uint32_t (&acc)[P][4], const uint64_t* __restrict__ sp,
+                                        int j, long long off, const uint32_t* __restrict__ tbl,
+                                        int len, unsigned long long r0m = 0, unsigned c0m = 0,
+                                        const uint2* lt = nullptr) {
+  uint4 x[U];
+  enc_load_group<U, MODE>(x, sp, j, off, len);
+  enc_fold_group<P, U, FL>(acc, x, j, tbl, r0m, c0m, lt);
 }
 
 // First-mismatch record of the verify kernels: key = column << 8 | row. Each

@@ -322,6 +322,15 @@ size_t lds_bytes(int k) {
 
 // XOR fast path (isal_hip_encmask) and LDS table halves only in the default
 // policy: XCD-contiguous order, nt buffer loads and stores.
+template <int P, int U, int FL>
+void launch_fl(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
+               const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long r0m,
+               unsigned c0m) {
+  const size_t lds = (FL & kEncLds) ? lds_bytes<P>(k) : 0;
+  hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, FL>), dim3(grid), dim3(kBlock), lds, s,
+                     ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+}
+
 template <int P, int U>
 void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
                 int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles,
@@ -330,18 +339,13 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufSC1NT, 2>>), dim3(grid), dim3(kBlock), 0, s,
                        ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
   else if (enc_order() == 2 && enc_lds(P, x) && x)
-    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncXor | kEncLds>), dim3(grid),
-                       dim3(kBlock), lds_bytes<P>(k), s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems,
-                       tiles, r0m, c0m);
+    launch_fl<P, U, kEncXor | kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
   else if (enc_order() == 2 && enc_lds(P, x))
-    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncLds>), dim3(grid), dim3(kBlock),
-                       lds_bytes<P>(k), s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
+    launch_fl<P, U, kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
   else if (enc_order() == 2 && x)
-    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, kEncXor>), dim3(grid), dim3(kBlock), 0,
-                       s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+    launch_fl<P, U, kEncXor>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
   else if (enc_order() == 2)
-    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>>), dim3(grid), dim3(kBlock), 0, s,
-                       ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
+    launch_fl<P, U, kEncLUT>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
   else
     hipLaunchKernelGGL((ec_encode_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
