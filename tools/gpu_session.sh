@@ -456,6 +456,9 @@ for s in $STEPS; do
                 run bench_$wl 300 python bench.py $args --cpu-seconds 5
                 cp "$OUT/bench_$wl.log" "$OUT/bench_$wl.json"
                 run rocprof_$wl 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$wl" -o $wl -- python3 bench.py $args --no-cpu-baseline
+                if [ $s = updateprof ]; then
+                        run steady_$wl 60 python3 tools/kernel_stats.py "$OUT/prof_$wl" "ec_update_v16<6>" --skip 5 --keep 20 --bytes 3489660928 --out "$OUT/update_update_kernel_steady.csv" --config "$cfg" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py $args --no-cpu-baseline"
+                fi
                 run pmc_fetch_$wl 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$wl" -o f -- python3 bench.py $args --no-cpu-baseline --steps 3 --warmup 1
                 run pmc_write_$wl 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$wl" -o w -- python3 bench.py $args --no-cpu-baseline --steps 3 --warmup 1
                 python3 tools/pmc_csv.py "$OUT/pmc_$wl.csv" "$cfg" "python bench.py $args --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_$wl" "$OUT/pmc_write_$wl" $kern
