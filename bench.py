@@ -262,9 +262,12 @@ def enc_kernel(rows: int, k: int, coef) -> str:
         lds = os.environ.get("ISAL_HIP_ENC_LDS")
         if lds == "1" or (lds != "0" and rows - (fl & 1) > 4 and rows <= 6):  # ec_kernels.hip enc_lds
             fl |= 2
-    st = 3 if os.environ.get("ISAL_HIP_ENC_STORE") == "1" and order == 2 else 2
-    base = f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, 2, {st}, {order}>"
-    return base + (f", {fl}>" if fl else ">")
+    if order == 2:
+        ld, st = 2, (3 if os.environ.get("ISAL_HIP_ENC_STORE") == "1" else 2)
+    else:
+        ld, st = 1, 1  # EncNT<U>: nt global loads and stores, tile-fastest
+    # rocprofv3 prints every template argument, the variant's default 0 too
+    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, {ld}, {st}, {order}>, {fl}>"
 
 
 def enc_group(k: int) -> int:
