@@ -84,72 +84,6 @@ __device__ __forceinline__ void encode_items(const uint64_t* __restrict__ ptrs, 
   }
 }
 
-// Split sources (stripes of two or more load groups, k >= 2U, k % U == 0):
-// a 512-lane workgroup covers one 4 KiB tile with two 256-lane halves; half g
-// folds load groups g, g + 2, ... of the sources, the upper half hands its
-// partial sums to the lower one through LDS, and the lower half stores. Each
-// lane then has one group's loads to wait for instead of two back to back,
-// and twice as many loads of a tile are in flight (round 4: k = 20 p = 6 had
-// two dependent load groups per lane at 4 waves per SIMD and idle VALU time).
-template <int P, class Pol, int FL>
-__device__ __forceinline__ void encode_items_split(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
-                                                   int dst0, const uint32_t* __restrict__ tbl, int len, int k,
-                                                   unsigned nitems, unsigned tiles, unsigned long long r0m,
-                                                   unsigned c0m) {
-  constexpr int U = Pol::U;
-  extern __shared__ uint2 enc_lt[];  // kEncLds: {a0, b0} of every coefficient of the pass
-  __shared__ uint32_t xch[P * 4 * kBlock];  // the upper half's partial sums, lane-contiguous
-  if constexpr ((FL & kEncLds) != 0) {
-    for (int i = threadIdx.x; i < k * P; i += 2 * kBlock) enc_lt[i] = make_uint2(tbl[i * kTbl], tbl[i * kTbl + 2]);
-    __syncthreads();
-  }
-  const int lane = threadIdx.x & (kBlock - 1), half = threadIdx.x / kBlock;
-  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
-    const unsigned per = nitems / 8;
-    const unsigned v = (nitems % 8) ? w : (w % 8) * per + w / 8;  // XCD-contiguous (order 2)
-    const unsigned stripe = v / tiles, tile = v - stripe * tiles;
-    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
-    const long long off = static_cast<long long>(tile) * kTile + lane * kVec;
-    const bool full = off + kVec <= len;
-    uint32_t acc[P][4];
-#pragma unroll
-    for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
-    if (full)
-      for (int j = half * U; j + U <= k; j += 2 * U)
-        chunk16<P, U, Pol::LD, FL>(acc, sp + src0, j, off, tbl, len, r0m, c0m, enc_lt);
-    if (half == 1 && full) {
-#pragma unroll
-      for (int l = 0; l < P; ++l)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) xch[(l * 4 + d) * kBlock + lane] = acc[l][d];
-    }
-    __syncthreads();
-    if (half == 0) {
-      if (full) {
-#pragma unroll
-        for (int l = 0; l < P; ++l)
-          store16<Pol::ST>(sp[dst0 + l], off,
-                           make_uint4(acc[l][0] ^ xch[(l * 4 + 0) * kBlock + lane],
-                                      acc[l][1] ^ xch[(l * 4 + 1) * kBlock + lane],
-                                      acc[l][2] ^ xch[(l * 4 + 2) * kBlock + lane],
-                                      acc[l][3] ^ xch[(l * 4 + 3) * kBlock + lane]),
-                           len);
-      } else if (off < len) {
-        dot_bytes<P>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off));
-      }
-    }
-    __syncthreads();  // xch is rewritten by the next item
-  }
-}
-
-template <int P, class Pol, int FL>
-__global__ __launch_bounds__(2 * kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encode_split(
-    const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
-    const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles,
-    unsigned long long r0m, unsigned c0m) {
-  encode_items_split<P, Pol, FL>(ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
-}
-
 template <int P, class Pol = EncDefault, int FL = kEncLUT>
 __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encode_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
@@ -388,24 +322,12 @@ size_t lds_bytes(int k) {
 
 // XOR fast path (isal_hip_encmask) and LDS table halves only in the default
 // policy: XCD-contiguous order, nt buffer loads and stores.
-// Split sources (ec_encode_split) for k >= 2U with k % U == 0 and load
-// groups of 8-12; ISAL_HIP_ENC_SPLIT=0 turns it off.
-bool enc_split(int k, int U) {
-  return U >= 8 && k >= 2 * U && k % U == 0 && isal_hip_knob(ISAL_HIP_KNOB_ENC_SPLIT) != 0;
-}
 
 template <int P, int U, int FL>
 void launch_fl(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
                const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long r0m,
                unsigned c0m) {
   const size_t lds = (FL & kEncLds) ? lds_bytes<P>(k) : 0;
-  if constexpr (U >= 8) {
-    if (enc_split(k, U)) {
-      hipLaunchKernelGGL((ec_encode_split<P, EncPol<U, kBufNT, kBufNT, 2>, FL>), dim3(grid), dim3(2 * kBlock),
-                         lds, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
-      return;
-    }
-  }
   hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, FL>), dim3(grid), dim3(kBlock), lds, s,
                      ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
 }

@@ -412,6 +412,39 @@ def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, l
         assert np.array_equal(out[l].cpu().numpy(), want[ns - 1][l]), l
 
 
+@pytest.mark.parametrize("k,rows,n,ns,gen", [
+    (20, 6, 65536 + 48, 5, "rs"),       # two groups of 10, XOR + LDS variant, ragged tail
+    (16, 4, 4096 * 3 + 16, 7, "rs"),    # two groups of 8, one-vector tail
+    (24, 8, 32768, 3, "rs"),            # two groups of 12, P = 8
+    (40, 3, 8192 + 4000, 4, "rs"),      # four groups of 10
+    (30, 1, 16384, 9, "rs"),            # three groups of 10 (odd), P = 1
+    (32, 5, 8192, 8, "big"),            # four groups of 8, no 0/1 structure
+    (20, 7, 4096, 2, "mask"),           # masks, a group that does not start at source 0
+    (36, 12, 8192, 3, "rs"),            # two passes (8 + 4 rows) of three groups of 12
+])
+def test_encode_load_groups_vs_oracle(engine, oracle, gpu, k, rows, n, ns, gen):
+    """Stripes of two or more load groups (enc_group: k a multiple of 8, 10 or
+    12 above it): batch encode == oracle with ragged tails, odd group counts
+    and two passes."""
+    import torch
+
+    if gen == "rs":
+        coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+    else:
+        coef = _coef_01(np.random.default_rng(k * 7 + rows), k, rows, gen)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 2000 + k + rows)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.encode(0)
+    torch.cuda.synchronize()
+    h_data, h_cod = _host(data), _host(coding)
+    want = _oracle_encode_all(oracle, coef, k, rows, [[h_data[s, j] for j in range(k)] for s in range(ns)])
+    for s in range(ns):
+        for l in range(rows):
+            assert np.array_equal(h_cod[s, l], want[s][l]), (s, l)
+    b.close()
+
+
 def test_xcd_item_order_update_and_checksums(engine, oracle, gpu, monkeypatch):
     """ISAL_HIP_XCD_ORDER=1 (update, checksum-only and fused CRC kernels take
     their items XCD-contiguously): item counts that are multiples of 8 (the

@@ -192,10 +192,10 @@ for s in $STEPS; do
                         run bench_$tag 300 python bench.py $args
                         cp "$OUT/bench_$tag.log" "$OUT/bench_$tag.json"
                         run rocprof_$tag 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$tag" -o $tag -- python3 bench.py $args
-                        run steady_$tag 60 python3 tools/kernel_stats.py "$OUT/prof_$tag" ec_encode_v16 --skip 5 --keep 20 --bytes $bytes --out "$OUT/${tag}_encode_kernel_steady.csv" --config "workload=encode k=$1 p=$2 len=$3 stripes=$4" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py $args"
+                        run steady_$tag 60 python3 tools/kernel_stats.py "$OUT/prof_$tag" ec_encode_ --skip 5 --keep 20 --bytes $bytes --out "$OUT/${tag}_encode_kernel_steady.csv" --config "workload=encode k=$1 p=$2 len=$3 stripes=$4" --command "rocprofv3 --kernel-trace --stats -- python3 bench.py $args"
                         run pmc_fetch_$tag 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$tag" -o f -- python3 bench.py $args --steps 3 --warmup 1
                         run pmc_write_$tag 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$tag" -o w -- python3 bench.py $args --steps 3 --warmup 1
-                        python3 tools/pmc_csv.py "$OUT/pmc_$tag.csv" "workload=encode k=$1 p=$2 len=$3 stripes=$4" "python bench.py $args --steps 3 --warmup 1" "$OUT/pmc_fetch_$tag" "$OUT/pmc_write_$tag" ec_encode_v16
+                        python3 tools/pmc_csv.py "$OUT/pmc_$tag.csv" "workload=encode k=$1 p=$2 len=$3 stripes=$4" "python bench.py $args --steps 3 --warmup 1" "$OUT/pmc_fetch_$tag" "$OUT/pmc_write_$tag" ec_encode_
                         run pmc_sq_$tag 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_$tag" -o s -- python3 bench.py $args --steps 2 --warmup 1
                 done
                 ;;
