@@ -272,6 +272,9 @@ def enc_kernel(rows: int, k: int, coef) -> str:
 
 def enc_group(k: int) -> int:
     """Sources per load group the engine launches with (ec_kernels.hip:enc_group)."""
+    force = os.environ.get("ISAL_HIP_ENC_GROUP", "")
+    if force in ("12", "10", "8", "6", "5", "4"):
+        return int(force)
     return next((u for u in (12, 10, 8, 6, 5, 4) if k >= u and k % u == 0), 4)
 
 

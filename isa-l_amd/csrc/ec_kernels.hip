@@ -280,6 +280,9 @@ unsigned grid_for(unsigned nitems) {
 // (all of a stripe's loads in flight at once for the common k), else 4.
 int enc_group(int k) {
   static const int cand[] = {12, 10, 8, 6, 5, 4};
+  const long long force = isal_hip_knob(ISAL_HIP_KNOB_ENC_GROUP);  // tuning A/B: one of cand
+  for (int u : cand)
+    if (force == u) return u;
   for (int u : cand)
     if (k >= u && k % u == 0) return u;
   return 4;

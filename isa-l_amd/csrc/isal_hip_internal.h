@@ -159,6 +159,7 @@ enum {
         ISAL_HIP_KNOB_KARG,            /* 0: device-resident drop-in encodes upload their arguments */
         ISAL_HIP_KNOB_MAX_HELPERS,     /* copy-out helper threads per process (default 8) */
         ISAL_HIP_KNOB_SYNC_SPIN,       /* 1: synchronous calls poll hipStreamQuery instead of blocking (A/B) */
+        ISAL_HIP_KNOB_ENC_GROUP,       /* 12/10/8/6/5/4: encode load group forced (tuning A/B) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

@@ -225,6 +225,17 @@ for s in $STEPS; do
                 run bench_decode 300 python bench.py --workload decode --no-cpu-baseline
                 ISAL_HIP_ENC_LDS=0 run bench_decode_lds0 300 python bench.py --workload decode --no-cpu-baseline
                 ;;
+        group)
+                # encode load group forced (ISAL_HIP_ENC_GROUP) x LDS halves, wide shapes
+                ISAL_HIP_ENC_GROUP=5 run pytest_gpu_group5 600 python -u -m pytest tests -m gpu -x -q -k "xor_fast_path or load_groups" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for v in ${GROUP_CASES:-10_8_1048576_1024_10_d 10_8_1048576_1024_5_d 10_8_1048576_1024_5_1 10_8_1048576_1024_10_1 20_6_4194304_64_10_d 20_6_4194304_64_5_d 20_6_4194304_64_4_d 10_4_1048576_1024_10_d 10_4_1048576_1024_5_d}; do
+                                set -- ${v//_/ }
+                                lds=$6; [ "$lds" = d ] && lds=
+                                ISAL_HIP_ENC_GROUP=$5 ISAL_HIP_ENC_LDS=$lds run bench_k$1p$2_g$5_l$6_r$r 300 python bench.py --workload encode --k $1 --p $2 --len $3 --stripes $4 --no-cpu-baseline
+                        done
+                done
+                ;;
         fuzzrss)
                 # the GPU differential fuzz target for 150 s with libFuzzer's 2 GiB RSS /
                 # malloc bounds; its status lines log the process RSS over time
