@@ -260,21 +260,26 @@ def enc_kernel(rows: int, k: int, coef) -> str:
                 and int(c[:, 0].max()) <= 1):
             fl |= 1
         lds = os.environ.get("ISAL_HIP_ENC_LDS")
-        if lds == "1" or (lds != "0" and rows - (fl & 1) > 4 and rows <= 6):  # ec_kernels.hip enc_lds
+        wide5 = os.environ.get("ISAL_HIP_ENC_WIDE5") != "0"
+        if lds == "1" or (lds != "0" and rows - (fl & 1) > 4
+                          and (rows <= 6 or (enc_group(k, rows) == 5 and wide5))):  # ec_kernels.hip enc_lds
             fl |= 2
     if order == 2:
         ld, st = 2, (3 if os.environ.get("ISAL_HIP_ENC_STORE") == "1" else 2)
     else:
         ld, st = 1, 1  # EncNT<U>: nt global loads and stores, tile-fastest
     # rocprofv3 prints every template argument, the variant's default 0 too
-    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k)}, {ld}, {st}, {order}>, {fl}>"
+    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, {ld}, {st}, {order}>, {fl}>"
 
 
-def enc_group(k: int) -> int:
-    """Sources per load group the engine launches with (ec_kernels.hip:enc_group)."""
+def enc_group(k: int, rows: int = 0) -> int:
+    """Sources per load group the engine launches with for a pass of `rows`
+    outputs (ec_kernels.hip:enc_group, enc_wide5)."""
     force = os.environ.get("ISAL_HIP_ENC_GROUP", "")
     if force in ("12", "10", "8", "6", "5", "4"):
         return int(force)
+    if rows >= 6 and k >= 10 and k % 5 == 0 and os.environ.get("ISAL_HIP_ENC_WIDE5") != "0":
+        return 5
     return next((u for u in (12, 10, 8, 6, 5, 4) if k >= u and k % u == 0), 4)
 
 

@@ -231,6 +231,51 @@ __device__ __forceinline__ void update_items(const uint64_t* __restrict__ ptrs, 
   }
 }
 
+// The drop-in call's single stripe, 4 bytes of every shard per lane instead
+// of 16 (ISAL_HIP_KARG_NARROW): a C2 stripe is then 1024 workgroups (16 waves
+// per CU) instead of 256 (4 per CU), so one call's loads and lookups overlap
+// across waves rather than running back to back in one wave per SIMD.
+__device__ __forceinline__ uint32_t load4nt(uint64_t base, long long off, int len) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
+  return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(off), 0, 2 /* nt */));
+}
+
+__device__ __forceinline__ void store4nt(uint64_t base, long long off, uint32_t v, int len) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(v), rs, static_cast<int>(off), 0, 2 /* nt */);
+}
+
+template <int P>
+__device__ __forceinline__ void fold4(uint32_t (&acc)[P], uint32_t x, const uint32_t* __restrict__ t) {
+  const Sel s = split(x);
+#pragma unroll
+  for (int l = 0; l < P; ++l) acc[l] ^= gf_mul4(load_coef(t + l * kTbl), s);
+}
+
+template <int P>
+__global__ __launch_bounds__(kBlock) void ec_encode_karg4(const isal_hip_karg a, int len, int k) {
+  const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
+  const long long off = (static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x) * 4;
+  if (off + 4 <= len) {
+    uint32_t acc[P];
+#pragma unroll
+    for (int l = 0; l < P; ++l) acc[l] = 0;
+    int j = 0;
+    for (; j + 8 <= k; j += 8) {
+      uint32_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = load4nt(ka->ptrs[j + u], off, len);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) fold4<P>(acc, x[u], ka->tbl + (j + u) * P * kTbl);
+    }
+    for (; j < k; ++j) fold4<P>(acc, load4nt(ka->ptrs[j], off, len), ka->tbl + j * P * kTbl);
+#pragma unroll
+    for (int l = 0; l < P; ++l) store4nt(ka->ptrs[k + l], off, acc[l], len);
+  } else if (off < len) {
+    dot_bytes<P>(ka->ptrs, 0, k, ka->tbl, k, off, static_cast<int>(len - off));
+  }
+}
+
 template <int P>
 __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restrict__ ptrs,
                                                         int ptr_stride, int src_idx, int dst0,
@@ -276,13 +321,26 @@ unsigned grid_for(unsigned nitems) {
   return (cap && nitems > cap) ? cap : nitems;
 }
 
+// Passes of 6-8 rows over k = 10, 15, 20, ... sources load in groups of 5
+// (ISAL_HIP_ENC_WIDE5=0 off): the smaller group leaves the registers for a
+// wave more per SIMD, and lets 7-8 row passes take the LDS table halves
+// without dropping to 3 waves. Same-box A/B, two runs each
+// (profiles/r04_group_ab.jsonl): k10p8 0.702 -> 0.714 (groups of 5 + LDS),
+// k20p6 0.649 -> 0.657; C2 (4 rows) 0.780 -> 0.772 with 5, so narrower passes
+// keep the large group.
+bool enc_wide5(int k, int P) {
+  return P >= 6 && k >= 10 && k % 5 == 0 && isal_hip_knob(ISAL_HIP_KNOB_ENC_WIDE5) != 0;
+}
+
 // Load-group size for k sources: the largest of {12,10,8,6,5,4} dividing k
-// (all of a stripe's loads in flight at once for the common k), else 4.
-int enc_group(int k) {
+// (all of a stripe's loads in flight at once for the common k), else 4;
+// P = the pass's rows (0: not known, the drop-in kernel-argument launch).
+int enc_group(int k, int P = 0) {
   static const int cand[] = {12, 10, 8, 6, 5, 4};
   const long long force = isal_hip_knob(ISAL_HIP_KNOB_ENC_GROUP);  // tuning A/B: one of cand
   for (int u : cand)
     if (force == u) return u;
+  if (enc_wide5(k, P)) return 5;
   for (int u : cand)
     if (k >= u && k % u == 0) return u;
   return 4;
@@ -310,12 +368,12 @@ bool enc_store_sc1() {
 // 8 TB/s, k10p6 0.752 -> 0.754, C2 0.7705 -> 0.7695, k10p8 0.715 -> 0.702,
 // decode (p = 3) 0.742 -> 0.744. It pays where pairing from SGPRs is not
 // possible (more than 4 looked-up rows) and the pass is not so wide that 3
-// waves per SIMD starve it: 5-6 rows. ISAL_HIP_ENC_LDS=1 forces it for every
-// width, =0 turns it off.
-bool enc_lds(int P, bool x) {
+// waves per SIMD starve it: 5-6 rows, and 7-8 rows loading in groups of 5
+// (enc_wide5). ISAL_HIP_ENC_LDS=1 forces it for every width, =0 turns it off.
+bool enc_lds(int P, bool x, int U) {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_LDS);
   if (v == 0 || v == 1) return v == 1;
-  return P - (x ? 1 : 0) > 4 && P <= 6;
+  return P - (x ? 1 : 0) > 4 && (P <= 6 || (U == 5 && isal_hip_knob(ISAL_HIP_KNOB_ENC_WIDE5) != 0));
 }
 
 template <int P>
@@ -342,9 +400,9 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
   if (enc_order() == 2 && enc_store_sc1())
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufSC1NT, 2>>), dim3(grid), dim3(kBlock), 0, s,
                        ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
-  else if (enc_order() == 2 && enc_lds(P, x) && x)
+  else if (enc_order() == 2 && enc_lds(P, x, U) && x)
     launch_fl<P, U, kEncXor | kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
-  else if (enc_order() == 2 && enc_lds(P, x))
+  else if (enc_order() == 2 && enc_lds(P, x, U))
     launch_fl<P, U, kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
   else if (enc_order() == 2 && x)
     launch_fl<P, U, kEncXor>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
@@ -364,7 +422,7 @@ hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
   const unsigned nitems = nstripes * tiles;
   const unsigned grid = grid_for(nitems);
   if (vec16) {
-    switch (enc_group(k)) {
+    switch (enc_group(k, P)) {
 #define EC_GROUP(u)                                                                                   \
   case u:                                                                                             \
     launch_v16<P, u>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, x, r0m, c0m); \
@@ -440,6 +498,14 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
   return 0;
 }
 
+// ISAL_HIP_KARG_NARROW: 1 = always the 4-byte-lane kernel, 0 = never;
+// default = shards up to 4 MiB (larger calls fill the GPU with 16-byte lanes).
+static bool karg_narrow(int len) {
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_KARG_NARROW);
+  if (v >= 0) return v != 0;
+  return len <= (4 << 20);
+}
+
 extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int k, int rows,
                                            const isal_hip_encmask* em, void* stream) {
   if (len <= 0 || rows <= 0) return 0;
@@ -447,6 +513,20 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int 
       static_cast<size_t>(kTbl) * k * rows > ISAL_HIP_KARG_TBL)
     return static_cast<int>(hipErrorInvalidValue);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (karg_narrow(len)) {
+    const unsigned blocks = static_cast<unsigned>((static_cast<long long>(len) + 4 * kBlock - 1) / (4 * kBlock));
+    switch (rows) {
+#define EC_KARG4(n)                                                                                           \
+  case n:                                                                                                     \
+    hipLaunchKernelGGL((ec_encode_karg4<n>), dim3(blocks), dim3(kBlock), 0, s, *a, len, k);                  \
+    break;
+      EC_KARG4(1) EC_KARG4(2) EC_KARG4(3) EC_KARG4(4) EC_KARG4(5) EC_KARG4(6) EC_KARG4(7) EC_KARG4(8)
+#undef EC_KARG4
+      default: return static_cast<int>(hipErrorInvalidValue);
+    }
+    isal_hip_count_launch();
+    return static_cast<int>(hipGetLastError());
+  }
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + kTile - 1) / kTile);
   const bool x = em && (em->ok & 1u);
   const unsigned long long r0m = x ? em->r0[0] : 0ull;

@@ -160,6 +160,8 @@ enum {
         ISAL_HIP_KNOB_MAX_HELPERS,     /* copy-out helper threads per process (default 8) */
         ISAL_HIP_KNOB_SYNC_SPIN,       /* 1: synchronous calls poll hipStreamQuery instead of blocking (A/B) */
         ISAL_HIP_KNOB_ENC_GROUP,       /* 12/10/8/6/5/4: encode load group forced (tuning A/B) */
+        ISAL_HIP_KNOB_KARG_NARROW,     /* drop-in kernel-argument encode with 4-byte lanes: 1 on, 0 off */
+        ISAL_HIP_KNOB_ENC_WIDE5,       /* 0: 6-8 row passes keep the largest load group (no groups of 5) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

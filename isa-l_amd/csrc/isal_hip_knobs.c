@@ -61,6 +61,8 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_MAX_HELPERS] = {"ISAL_HIP_MAX_HELPERS", NULL},
         [ISAL_HIP_KNOB_SYNC_SPIN] = {"ISAL_HIP_SYNC_SPIN", NULL},
         [ISAL_HIP_KNOB_ENC_GROUP] = {"ISAL_HIP_ENC_GROUP", NULL},
+        [ISAL_HIP_KNOB_KARG_NARROW] = {"ISAL_HIP_KARG_NARROW", NULL},
+        [ISAL_HIP_KNOB_ENC_WIDE5] = {"ISAL_HIP_ENC_WIDE5", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];

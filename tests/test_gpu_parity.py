@@ -445,6 +445,48 @@ def test_encode_load_groups_vs_oracle(engine, oracle, gpu, k, rows, n, ns, gen):
     b.close()
 
 
+@pytest.mark.parametrize("narrow", ["1", "0"])
+@pytest.mark.parametrize("k,rows,n", [
+    (10, 4, 1 << 20),      # C2 stripe
+    (10, 4, 16),           # shortest kernel-argument call: one lane
+    (10, 4, 4096 * 3 + 7), # ragged tail: 3 bytes past the last full lane dword
+    (13, 5, 8192 + 12),    # k % 8: the remainder loop
+    (29, 3, 4096),         # k + rows = 32 pointers (the kernel-argument limit)
+    (10, 8, 4096 + 4),     # 8 rows
+    (1, 1, 64),
+    (14, 6, 20000),        # 5 * k * rows = 420 of the 448 table dwords
+])
+def test_dropin_kernel_args_vs_oracle(engine, oracle, gpu, monkeypatch, capfd, narrow, k, rows, n):
+    """The drop-in call on 16-byte-aligned device shards passes its pointers and
+    tables as kernel arguments; its kernel takes 16 bytes per lane or, with
+    ISAL_HIP_KARG_NARROW (default for shards up to 4 MiB), 4 bytes per lane:
+    both == oracle, tails included, and the route log names the route."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", "gpu")
+    _setenv(monkeypatch, "ISAL_HIP_KARG_NARROW", narrow)
+    _setenv(monkeypatch, "ISAL_HIP_LOG", "1")
+    coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:] if rows > 1 else np.full(k, 3, dtype=np.uint8)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    stride = (n + 15) // 16 * 16 + 256
+    buf = torch.empty((k + rows) * stride, dtype=torch.uint8, device=gpu)
+    buf.random_(generator=torch.Generator(device=gpu).manual_seed(k * 1000 + n))
+    shard = lambda i: buf[i * stride: i * stride + n]  # noqa: E731
+    h = _host(buf)
+    src = [h[j * stride: j * stride + n] for j in range(k)]
+    canary = h[k * stride: (k + rows) * stride].copy()
+    want = oracle.encode(coef, k, rows, src)
+    capfd.readouterr()
+    engine.ec_encode_data(n, k, rows, tbls, [shard(j) for j in range(k)], [shard(k + l) for l in range(rows)])
+    torch.cuda.synchronize()
+    assert "kernel-args" in capfd.readouterr().err
+    out = _host(buf)
+    for l in range(rows):
+        base = (k + l) * stride
+        assert np.array_equal(out[base: base + n], want[l]), l
+        assert np.array_equal(out[base + n: base + stride], canary[l * stride + n: (l + 1) * stride]), l
+
+
 def test_xcd_item_order_update_and_checksums(engine, oracle, gpu, monkeypatch):
     """ISAL_HIP_XCD_ORDER=1 (update, checksum-only and fused CRC kernels take
     their items XCD-contiguously): item counts that are multiples of 8 (the

@@ -236,6 +236,31 @@ for s in $STEPS; do
                         done
                 done
                 ;;
+        narrow)
+                # drop-in kernel-argument encode with 4-byte lanes (ISAL_HIP_KARG_NARROW) A/B
+                run pytest_gpu_narrow 600 python -u -m pytest tests -m gpu -x -q -k "dropin or concurrent or golden or xor_fast_path" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for x in 0 1; do
+                                for t in 1 4 16; do
+                                        ISAL_HIP_KARG_NARROW=$x run dropin_n${x}_t${t}_r$r 120 tools/dropin_bench 10 4 1048576 64 $t 3
+                                done
+                                ISAL_HIP_KARG_NARROW=$x run dropin_n${x}_small_r$r 120 tools/dropin_bench 10 4 4096 64 1 3
+                                ISAL_HIP_KARG_NARROW=$x run dropin_n${x}_4m_r$r 120 tools/dropin_bench 10 4 4194304 16 1 3
+                        done
+                done
+                ;;
+        wide5)
+                # 6-8 row passes in load groups of 5 (ISAL_HIP_ENC_WIDE5) A/B
+                run pytest_gpu_wide5 600 python -u -m pytest tests -m gpu -x -q -k "xor_fast_path or load_groups or random_shapes or maximum_stripe or decode" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for shape in ${WIDE5_SHAPES:-10_6_1048576_1024 10_7_1048576_1024 10_8_1048576_1024 20_6_4194304_64 20_8_4194304_64 15_6_1048576_1024 30_6_1048576_512}; do
+                                set -- ${shape//_/ }
+                                for x in 0 1; do
+                                        ISAL_HIP_ENC_WIDE5=$x run bench_k$1p$2_w${x}_r$r 300 python bench.py --workload encode --k $1 --p $2 --len $3 --stripes $4 --no-cpu-baseline
+                                done
+                        done
+                done
+                ;;
         fuzzrss)
                 # the GPU differential fuzz target for 150 s with libFuzzer's 2 GiB RSS /
                 # malloc bounds; its status lines log the process RSS over time
