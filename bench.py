@@ -272,6 +272,30 @@ def enc_kernel(rows: int, k: int, coef) -> str:
     return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, {ld}, {st}, {order}>, {fl}>"
 
 
+def copy_ceiling(dev, nbytes: int = 2 << 30, reps: int = 10) -> dict:
+    """Achievable HBM rate on this GPU: a device-to-device copy of `nbytes`
+    (hipMemcpyAsync's copy kernel through torch), HIP events around `reps`
+    copies after warm-up, read + write bytes counted."""
+    import torch
+
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    src.fill_(0x5A)
+    for _ in range(3):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    s = e0.elapsed_time(e1) / 1e3 / reps
+    del src, dst
+    gbs = 2 * nbytes / s / 1e9
+    return {"kernel": "device-to-device copy (torch Tensor.copy_), 2 GiB", "gb_s": round(gbs, 1),
+            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+
+
 def enc_group(k: int, rows: int = 0) -> int:
     """Sources per load group the engine launches with for a pass of `rows`
     outputs (ec_kernels.hip:enc_group, enc_wide5)."""
@@ -1134,6 +1158,11 @@ def main(argv=None):
         result["roofline"]["profile_launch_ms"] = round(prof[0], 4)
         result["roofline"]["profile_frac"] = round(bytes_per_launch / (prof[0] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
         result["roofline"]["kernel_stats_source"] = prof[1]
+    if d.world == 1:
+        # the achievable peak, measured live with a device copy
+        cc = copy_ceiling(dev)
+        result["roofline"]["copy_ceiling"] = cc
+        result["roofline"]["frac_of_copy_ceiling"] = round(achieved / cc["gb_s"], 4)
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))

@@ -325,9 +325,11 @@ unsigned grid_for(unsigned nitems) {
 // (ISAL_HIP_ENC_WIDE5=0 off): the smaller group leaves the registers for a
 // wave more per SIMD, and lets 7-8 row passes take the LDS table halves
 // without dropping to 3 waves. Same-box A/B, two runs each
-// (profiles/r04_group_ab.jsonl): k10p8 0.702 -> 0.714 (groups of 5 + LDS),
-// k20p6 0.649 -> 0.657; C2 (4 rows) 0.780 -> 0.772 with 5, so narrower passes
-// keep the large group.
+// (profiles/r04_wide5_ab.jsonl): k10p6 0.753 -> 0.766 of 8 TB/s, k10p7
+// 0.741 -> 0.747, k10p8 0.721 -> 0.732, k20p6 0.663 -> 0.670, k20p8 0.564 ->
+// 0.591, k30p6 0.673 -> 0.680, k15p6 (already 5) flat; C2 (4 rows) 0.780 ->
+// 0.772 with 5 (profiles/r04_group_ab.jsonl), so narrower passes keep the
+// large group.
 bool enc_wide5(int k, int P) {
   return P >= 6 && k >= 10 && k % 5 == 0 && isal_hip_knob(ISAL_HIP_KNOB_ENC_WIDE5) != 0;
 }
@@ -499,11 +501,14 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
 }
 
 // ISAL_HIP_KARG_NARROW: 1 = always the 4-byte-lane kernel, 0 = never;
-// default = shards up to 4 MiB (larger calls fill the GPU with 16-byte lanes).
+// default = shards up to 1 MiB. C2 stripes, same box, two runs each
+// (profiles/r04_karg_narrow_ab.jsonl): 16 threads 3098-3121 -> 3312-3326 GiB/s,
+// 1 thread 18.2 -> 17.9 us per call, 4 KiB shards flat; 4 MiB shards
+// 24.4 -> 27.0 us (4x the load instructions once the call fills the GPU).
 static bool karg_narrow(int len) {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_KARG_NARROW);
   if (v >= 0) return v != 0;
-  return len <= (4 << 20);
+  return len <= (1 << 20);
 }
 
 extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int k, int rows,

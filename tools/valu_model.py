@@ -27,12 +27,19 @@ COPY_CEILING = 6.29e12  # B/s, float4 copy (MI355X_MICROARCH.md)
 SHAPES = [
     ("C2 k10p4", "r04_pmc_sq_c2.txt", None, "ec_encode_v16<4, EncPol<10, 2, 2, 2>, 1>", 10, 4, 1 << 20, 1024, True,
      "r04_c2_encode_kernel_steady.csv"),
-    ("k10p6", "r04_pmc_sq_wide.txt", "## k10p6", "ec_encode_v16<6, EncPol<10, 2, 2, 2>, 3>", 10, 6, 1 << 20, 1024, True,
+    ("k10p6", "r04_pmc_sq_wide.txt", "## k10p6", "ec_encode_v16<6, EncPol<5, 2, 2, 2>, 3>", 10, 6, 1 << 20, 1024, True,
      "r04_k10p6_encode_kernel_steady.csv"),
-    ("k10p8", "r04_pmc_sq_wide.txt", "## k10p8", "ec_encode_v16<8, EncPol<10, 2, 2, 2>, 1>", 10, 8, 1 << 20, 1024, True,
+    ("k10p8", "r04_pmc_sq_wide.txt", "## k10p8", "ec_encode_v16<8, EncPol<5, 2, 2, 2>, 3>", 10, 8, 1 << 20, 1024, True,
      "r04_k10p8_encode_kernel_steady.csv"),
-    ("k20p6", "r04_pmc_sq_wide.txt", "## k20p6", "ec_encode_v16<6, EncPol<10, 2, 2, 2>, 3>", 20, 6, 4 << 20, 64, True,
+    ("k20p6", "r04_pmc_sq_wide.txt", "## k20p6", "ec_encode_v16<6, EncPol<5, 2, 2, 2>, 3>", 20, 6, 4 << 20, 64, True,
      "r04_k20p6_encode_kernel_steady.csv"),
+    # the same shapes with groups of 10 (ISAL_HIP_ENC_WIDE5=0; another box)
+    ("k10p6 g10", "r04_pmc_sq_wide_g10.txt", "## k10p6", "ec_encode_v16<6, EncPol<10, 2, 2, 2>, 3>", 10, 6, 1 << 20,
+     1024, True, "r04_k10p6_encode_g10_kernel_steady.csv"),
+    ("k10p8 g10", "r04_pmc_sq_wide_g10.txt", "## k10p8", "ec_encode_v16<8, EncPol<10, 2, 2, 2>, 1>", 10, 8, 1 << 20,
+     1024, True, "r04_k10p8_encode_g10_kernel_steady.csv"),
+    ("k20p6 g10", "r04_pmc_sq_wide_g10.txt", "## k20p6", "ec_encode_v16<6, EncPol<10, 2, 2, 2>, 3>", 20, 6, 4 << 20,
+     64, True, "r04_k20p6_encode_g10_kernel_steady.csv"),
 ]
 
 
