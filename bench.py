@@ -248,8 +248,10 @@ def enc_kernel(rows: int, k: int, coef) -> str:
     (enc_group), work order (enc_order) and variant — bit 0 the XOR path for
     0/1 rows and columns (isal_hip_enc_masks: row 0 and column 0 hold only
     0/1, k <= 64; ISAL_HIP_ENC_XOR=0 off), bit 1 low table halves from LDS
-    (5-6 looked-up rows; ISAL_HIP_ENC_LDS=1 always, =0 never); both only in
-    the default order-2 policy."""
+    (more than 4 looked-up rows in passes of up to 6 rows, or of 7-8 rows
+    loading in groups of 5; ISAL_HIP_ENC_LDS=1 always, =0 never); both only in
+    the default order-2 policy. The library names the same instantiation on
+    stderr with ISAL_HIP_LOG=2."""
     import numpy as np
 
     c = np.asarray(coef, dtype=np.uint8).reshape(rows, k)
@@ -267,33 +269,49 @@ def enc_kernel(rows: int, k: int, coef) -> str:
     if order == 2:
         ld, st = 2, (3 if os.environ.get("ISAL_HIP_ENC_STORE") == "1" else 2)
     else:
-        ld, st = 1, 1  # EncNT<U>: nt global loads and stores, tile-fastest
+        ld, st = 2, 2  # EncNT<U> = EncPol<U>: nt buffer loads and stores, tile-fastest
     # rocprofv3 prints every template argument, the variant's default 0 too
     return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, {ld}, {st}, {order}>, {fl}>"
 
 
 def copy_ceiling(dev, nbytes: int = 2 << 30, reps: int = 10) -> dict:
-    """Achievable HBM rate on this GPU: a device-to-device copy of `nbytes`
-    (hipMemcpyAsync's copy kernel through torch), HIP events around `reps`
-    copies after warm-up, read + write bytes counted."""
+    """Achievable HBM rate on this GPU: tools/copy_probe.hip,
+    the encode's memory skeleton without arithmetic (16 B per lane, nt buffer
+    loads and stores, XCD-contiguous 4 KiB tiles), copying `nbytes` `reps`
+    times, HIP events on its stream, read + write bytes counted. Falls back to
+    torch's device copy (named as such) when the probe is not built."""
+    import ctypes
+
     import torch
 
     src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     dst = torch.empty_like(src)
     src.fill_(0x5A)
-    for _ in range(3):
-        dst.copy_(src)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        dst.copy_(src)
-    e1.record()
     torch.cuda.synchronize(dev)
-    s = e0.elapsed_time(e1) / 1e3 / reps
+    so = os.path.join(REPO, "tools", "libcopy_probe.so")
+    if os.path.exists(so):
+        lib = ctypes.CDLL(so)
+        lib.copy_probe_gbs.restype = ctypes.c_double
+        lib.copy_probe_gbs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulonglong, ctypes.c_int]
+        gbs = lib.copy_probe_gbs(dst.data_ptr(), src.data_ptr(), nbytes, reps)
+        if gbs <= 0:
+            raise RuntimeError(f"copy probe failed ({gbs})")
+        ok = bool(torch.equal(dst[:1 << 20], src[:1 << 20]) and torch.equal(dst[-(1 << 20):], src[-(1 << 20):]))
+        name = "copy_tiles (tools/copy_probe.hip: 16 B/lane nt buffer load+store, 4 KiB tiles), 2 GiB"
+    else:
+        for _ in range(3):
+            dst.copy_(src)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            dst.copy_(src)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        gbs = 2 * nbytes / (e0.elapsed_time(e1) / 1e3 / reps) / 1e9
+        ok = True
+        name = "device-to-device copy (torch Tensor.copy_; tools/libcopy_probe.so not built), 2 GiB"
     del src, dst
-    gbs = 2 * nbytes / s / 1e9
-    return {"kernel": "device-to-device copy (torch Tensor.copy_), 2 GiB", "gb_s": round(gbs, 1),
-            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+    return {"kernel": name, "gb_s": round(gbs, 1), "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4), "copy_ok": ok}
 
 
 def enc_group(k: int, rows: int = 0) -> int:

@@ -24,6 +24,7 @@
 //    never touching bytes outside [ptr, ptr+len)).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 
@@ -386,10 +387,21 @@ size_t lds_bytes(int k) {
 // XOR fast path (isal_hip_encmask) and LDS table halves only in the default
 // policy: XCD-contiguous order, nt buffer loads and stores.
 
+// ISAL_HIP_LOG=2: name each vector encode launch the way rocprofv3 prints it
+// (bench.py's roofline.kernel must name the same instantiation;
+// test_bench_kernel_label_matches_launch).
+template <int P, class Pol, int FL>
+void log_launch() {
+  if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2)
+    fprintf(stderr, "isal_hip: kernel ec_encode_v16<%d, EncPol<%d, %d, %d, %d>, %d>\n", P, Pol::U, Pol::LD, Pol::ST,
+            Pol::ORDER, FL);
+}
+
 template <int P, int U, int FL>
 void launch_fl(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
                const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long r0m,
                unsigned c0m) {
+  log_launch<P, EncPol<U, kBufNT, kBufNT, 2>, FL>();
   const size_t lds = (FL & kEncLds) ? lds_bytes<P>(k) : 0;
   hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, FL>), dim3(grid), dim3(kBlock), lds, s,
                      ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
@@ -399,10 +411,11 @@ template <int P, int U>
 void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
                 int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles,
                 bool x, unsigned long long r0m, unsigned c0m) {
-  if (enc_order() == 2 && enc_store_sc1())
+  if (enc_order() == 2 && enc_store_sc1()) {
+    log_launch<P, EncPol<U, kBufNT, kBufSC1NT, 2>, 0>();
     hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufSC1NT, 2>>), dim3(grid), dim3(kBlock), 0, s,
                        ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
-  else if (enc_order() == 2 && enc_lds(P, x, U) && x)
+  } else if (enc_order() == 2 && enc_lds(P, x, U) && x)
     launch_fl<P, U, kEncXor | kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
   else if (enc_order() == 2 && enc_lds(P, x, U))
     launch_fl<P, U, kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
@@ -410,9 +423,11 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
     launch_fl<P, U, kEncXor>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
   else if (enc_order() == 2)
     launch_fl<P, U, kEncLUT>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
-  else
+  else {
+    log_launch<P, EncNT<U>, 0>();
     hipLaunchKernelGGL((ec_encode_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
+  }
 }
 
 template <int P>

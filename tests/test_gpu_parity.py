@@ -1928,6 +1928,35 @@ def test_bench_rccl_control_plane_single_rank(gpu):
         assert out["rccl_world_size"] == 1 and out["rank_devices"][0]["pci"], out
 
 
+@pytest.mark.parametrize("args,env", [
+    (["--k", "10", "--p", "4"], {}),                                  # C2 shape: XOR path, groups of 10
+    (["--k", "10", "--p", "8"], {}),                                  # 8 rows: groups of 5 + LDS halves
+    (["--k", "20", "--p", "6", "--len", "262144", "--stripes", "8"], {}),
+    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_WIDE5": "0"}),
+    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_LDS": "0", "ISAL_HIP_ENC_XOR": "0"}),
+    (["--k", "12", "--p", "5"], {"ISAL_HIP_ENC_GROUP": "4"}),
+    (["--k", "10", "--p", "4"], {"ISAL_HIP_ENC_ORDER": "0"}),
+    (["--k", "10", "--p", "4"], {"ISAL_HIP_ENC_STORE": "1"}),
+    (["--workload", "decode"], {}),
+])
+def test_bench_kernel_label_matches_launch(gpu, args, env):
+    """bench.py's roofline.kernel (the name its PMC / steady-state profile files
+    are looked up by) is the instantiation the library launched, as the library
+    itself names it under ISAL_HIP_LOG=2."""
+    import json
+    import sys
+
+    base = ["--len", "65536", "--stripes", "16"] if "--len" not in args else []
+    cmd = [sys.executable, os.path.join(ecutil.REPO, "bench.py"), "--workload", "encode", "--steps", "1",
+           "--warmup", "1", "--no-cpu-baseline"] + base + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ecutil.REPO,
+                       env={**os.environ, "ISAL_HIP_LOG": "2", **env})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    launched = {l.split("kernel ", 1)[1] for l in r.stderr.splitlines() if l.startswith("isal_hip: kernel ")}
+    assert out["roofline"]["kernel"] in launched, (out["roofline"]["kernel"], launched)
+
+
 def test_multi_device_encode_host_stripes_vs_oracle(engine, oracle, gpu):
     """isal_hip_multi_*: host stripes over every visible GPU (here: one), each
     GPU its contiguous range through its own pipeline; == oracle."""

@@ -1,0 +1,63 @@
+// copy_probe.hip — the achievable HBM rate on this GPU, for bench.py's
+// roofline.copy_ceiling ("also measure achievable peak with a
+// device copy kernel, and report both"). Measurement infrastructure, not part
+// of libisal_hip.so: built by `make -C isa-l_amd tools` into
+// tools/libcopy_probe.so and loaded by bench.py through ctypes after torch.
+//
+// The kernel is the encode's memory skeleton with no arithmetic: each lane
+// moves 16 bytes per 4 KiB tile with non-temporal buffer loads and stores (the
+// encode's access mode), one tile per workgroup, tiles handed out
+// XCD-contiguously as the encode does. MI355X_MICROARCH.md quotes 6.29 TB/s for
+// a float4 copy.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kTile = kBlock * 16;
+
+__global__ __launch_bounds__(kBlock) void copy_tiles(uint64_t dst, uint64_t src, unsigned ntiles, int chunk) {
+  const unsigned per = ntiles / 8;
+  const unsigned w = blockIdx.x;
+  const unsigned t = (ntiles % 8) ? w : (w % 8) * per + w / 8;
+  const long long base = static_cast<long long>(t) * kTile;
+  // one buffer descriptor per chunk of at most 1 GiB so the 32-bit offset fits
+  const long long cbase = base / chunk * chunk;
+  const int off = static_cast<int>(base - cbase) + threadIdx.x * 16;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(src + cbase), 0, chunk, 0x00020000);
+  const auto rd = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(dst + cbase), 0, chunk, 0x00020000);
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const v4i v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2 /* nt */);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rd, off, 0, 2 /* nt */);
+}
+
+}  // namespace
+
+// Copies n bytes (a multiple of 4 KiB, at most 2^40) from src to dst `reps`
+// times after two warm-up copies, on a stream of its own; returns the copy
+// rate in GB/s (read + write bytes), or a negative HIP error code.
+extern "C" double copy_probe_gbs(void* dst, const void* src, unsigned long long n, int reps) {
+  if (n == 0 || n % kTile || reps <= 0) return -1.0;
+  const unsigned ntiles = static_cast<unsigned>(n / kTile);
+  const int chunk = 1 << 30;
+  hipStream_t s;
+  hipEvent_t e0, e1;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -2.0;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int i = 0; i < reps + 2; ++i) {
+    if (i == 2) hipEventRecord(e0, s);
+    hipLaunchKernelGGL(copy_tiles, dim3(ntiles), dim3(kBlock), 0, s, reinterpret_cast<uint64_t>(dst),
+                       reinterpret_cast<uint64_t>(src), ntiles, chunk);
+  }
+  hipEventRecord(e1, s);
+  const hipError_t err = hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipStreamDestroy(s);
+  if (err != hipSuccess || ms <= 0.f) return -3.0;
+  return 2.0 * static_cast<double>(n) * reps / (ms * 1e-3) / 1e9;
+}

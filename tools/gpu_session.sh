@@ -261,6 +261,9 @@ for s in $STEPS; do
                         done
                 done
                 ;;
+        labels)
+                run pytest_gpu_labels 900 python -u -m pytest tests -m gpu -x -v -k "kernel_label or dropin_kernel_args or smoke" --timeout 300 --timeout-method thread
+                ;;
         fuzzrss)
                 # the GPU differential fuzz target for 150 s with libFuzzer's 2 GiB RSS /
                 # malloc bounds; its status lines log the process RSS over time
