@@ -387,6 +387,22 @@ size_t lds_bytes(int k) {
 // XOR fast path (isal_hip_encmask) and LDS table halves only in the default
 // policy: XCD-contiguous order, nt buffer loads and stores.
 
+// Dynamic LDS each vector-encode workgroup of a pass of at most 4 rows
+// allocates: what it uses, at least 32 KiB — an occupancy cap of 5 workgroups
+// (5 waves per SIMD) per CU, whose 160 KiB of LDS the workgroups share. The
+// narrow passes' kernels fit 6-8 waves per SIMD by their registers and run
+// faster capped, same box, two runs each (profiles/r04_occupancy_ab.jsonl,
+// r04_ldsmin_ab.jsonl): C3 decode 0.742-0.746 -> 0.754-0.756 of 8 TB/s,
+// k10p1 0.728 -> 0.748, k10p2 0.731 -> 0.757, k4p2 0.780 -> 0.798, C2 flat;
+// wider passes (4-5 waves by their registers) measured flat to 2 % slower
+// with it (k20p6 0.679 -> 0.664), so they allocate only what they use.
+// ISAL_HIP_ENC_LDS_MIN=bytes sets the minimum for every width, 0 = none.
+size_t enc_lds_alloc(size_t used, int P) {
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_LDS_MIN);
+  const size_t min = v < 0 ? (P <= 4 ? 32768 : 0) : (v <= 65536 ? static_cast<size_t>(v) : 0);
+  return used > min ? used : min;
+}
+
 // ISAL_HIP_LOG=2: name each vector encode launch the way rocprofv3 prints it
 // (bench.py's roofline.kernel must name the same instantiation;
 // test_bench_kernel_label_matches_launch).
@@ -402,7 +418,7 @@ void launch_fl(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_strid
                const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long r0m,
                unsigned c0m) {
   log_launch<P, EncPol<U, kBufNT, kBufNT, 2>, FL>();
-  const size_t lds = (FL & kEncLds) ? lds_bytes<P>(k) : 0;
+  const size_t lds = enc_lds_alloc((FL & kEncLds) ? lds_bytes<P>(k) : 0, P);
   hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, FL>), dim3(grid), dim3(kBlock), lds, s,
                      ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
 }
@@ -462,8 +478,12 @@ hipError_t update_pass(const uint64_t* ptrs, int ptr_stride, int src_idx, int ds
   const unsigned span = vec16 ? kTile : kBlock;
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
   const unsigned nitems = nstripes * tiles;
+  // ISAL_HIP_UPD_LDS_MIN=bytes: dynamic LDS per update workgroup, an occupancy
+  // cap for A/B runs (as enc_lds_alloc; default none)
+  const long long um = isal_hip_knob(ISAL_HIP_KNOB_UPD_LDS_MIN);
+  const size_t ulds = um > 0 && um <= 65536 ? static_cast<size_t>(um) : 0;
   if (vec16)
-    hipLaunchKernelGGL(ec_update_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
+    hipLaunchKernelGGL(ec_update_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), ulds, s, ptrs,
                        ptr_stride, src_idx, dst0, tbl, len, nitems, tiles, xcd_order());
   else
     hipLaunchKernelGGL(ec_update_b1<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,

@@ -162,6 +162,8 @@ enum {
         ISAL_HIP_KNOB_ENC_GROUP,       /* 12/10/8/6/5/4: encode load group forced (tuning A/B) */
         ISAL_HIP_KNOB_KARG_NARROW,     /* drop-in kernel-argument encode with 4-byte lanes: 1 on, 0 off */
         ISAL_HIP_KNOB_ENC_WIDE5,       /* 0: 6-8 row passes keep the largest load group (no groups of 5) */
+        ISAL_HIP_KNOB_ENC_LDS_MIN,     /* minimum dynamic LDS per encode workgroup (default 32 KiB for <= 4 rows) */
+        ISAL_HIP_KNOB_UPD_LDS_MIN,     /* dynamic LDS per update workgroup: occupancy cap (A/B, default none) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

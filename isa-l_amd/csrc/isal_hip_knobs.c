@@ -63,6 +63,8 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_ENC_GROUP] = {"ISAL_HIP_ENC_GROUP", NULL},
         [ISAL_HIP_KNOB_KARG_NARROW] = {"ISAL_HIP_KARG_NARROW", NULL},
         [ISAL_HIP_KNOB_ENC_WIDE5] = {"ISAL_HIP_ENC_WIDE5", NULL},
+        [ISAL_HIP_KNOB_ENC_LDS_MIN] = {"ISAL_HIP_ENC_LDS_MIN", NULL},
+        [ISAL_HIP_KNOB_UPD_LDS_MIN] = {"ISAL_HIP_UPD_LDS_MIN", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];

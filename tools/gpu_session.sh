@@ -264,6 +264,60 @@ for s in $STEPS; do
         labels)
                 run pytest_gpu_labels 900 python -u -m pytest tests -m gpu -x -v -k "kernel_label or dropin_kernel_args or smoke" --timeout 300 --timeout-method thread
                 ;;
+        occ)
+                # occupancy cap through unused LDS per workgroup (ISAL_HIP_ENC_LDS_PAD)
+                for r in 1 2; do
+                        for pad in 0 22528 27136 32768 40960; do
+                                ISAL_HIP_ENC_LDS_MIN=$pad run bench_c2_pad${pad}_r$r 300 python bench.py --no-cpu-baseline
+                                ISAL_HIP_ENC_LDS_MIN=$pad run bench_decode_pad${pad}_r$r 300 python bench.py --workload decode --no-cpu-baseline
+                        done
+                done
+                ;;
+        ldsmin)
+                # encode occupancy cap (ISAL_HIP_ENC_LDS_MIN, default 32 KiB) vs none, per shape
+                run pytest_gpu_ldsmin 600 python -u -m pytest tests -m gpu -x -q -k "xor_fast_path or load_groups or random_shapes or decode or raid or golden" --timeout 300 --timeout-method thread
+                for r in 1 2; do
+                        for w in "encode --k 10 --p 4" "decode" "encode --k 10 --p 1" "encode --k 10 --p 2" "encode --k 10 --p 6" "encode --k 10 --p 8" "encode --k 20 --p 6 --len 4194304 --stripes 64" "encode --k 4 --p 2"; do
+                                tag=$(echo $w | tr -d ' -' | cut -c1-24)
+                                for m in 0 32768; do
+                                        ISAL_HIP_ENC_LDS_MIN=$m run bench_${tag}_m${m}_r$r 300 python bench.py --workload $w --no-cpu-baseline
+                                done
+                        done
+                done
+                ;;
+        updocc)
+                # update kernel occupancy cap (ISAL_HIP_UPD_LDS_MIN)
+                for r in 1 2; do
+                        for m in 0 22528 27136 32768 40960; do
+                                ISAL_HIP_UPD_LDS_MIN=$m run bench_update_m${m}_r$r 300 python bench.py --workload update --k 20 --p 6 --len 4194304 --stripes 64 --no-cpu-baseline
+                        done
+                done
+                ;;
+        confirm)
+                run pytest_gpu_confirm 600 python -u -m pytest tests -m gpu -x -q -k "xor_fast_path or load_groups or random_shapes or decode or raid or golden or kernel_label or smoke" --timeout 300 --timeout-method thread
+                for w in "encode" "decode" "encode --k 20 --p 6 --len 4194304 --stripes 64" "encode --k 10 --p 2" "encode --k 10 --p 8"; do
+                        tag=$(echo $w | tr -d ' -' | cut -c1-24)
+                        run bench_${tag}_default 300 python bench.py --workload $w --no-cpu-baseline
+                done
+                ;;
+        c2ab)
+                # C2 and C3 with the narrow-pass occupancy cap (default) and without
+                for r in 1 2 3; do
+                        for m in d 0; do
+                                v=$m; [ "$m" = d ] && v=
+                                ISAL_HIP_ENC_LDS_MIN=$v run bench_c2_m${m}_r$r 300 python bench.py --no-cpu-baseline
+                                ISAL_HIP_ENC_LDS_MIN=$v run bench_decode_m${m}_r$r 300 python bench.py --workload decode --no-cpu-baseline
+                        done
+                done
+                ;;
+        grid)
+                # grid-stride launches of at most n workgroups (ISAL_HIP_GRID_CAP)
+                for r in 1 2; do
+                        for cap in 0 2048 4096 8192 16384; do
+                                ISAL_HIP_GRID_CAP=$cap run bench_c2_cap${cap}_r$r 300 python bench.py --no-cpu-baseline
+                        done
+                done
+                ;;
         fuzzrss)
                 # the GPU differential fuzz target for 150 s with libFuzzer's 2 GiB RSS /
                 # malloc bounds; its status lines log the process RSS over time
