@@ -61,3 +61,22 @@ extern "C" double copy_probe_gbs(void* dst, const void* src, unsigned long long 
   if (err != hipSuccess || ms <= 0.f) return -3.0;
   return 2.0 * static_cast<double>(n) * reps / (ms * 1e-3) / 1e9;
 }
+
+// LDS bookkeeping for the encode's occupancy cap: the device's
+// LDS per CU, and how many 256-lane copy_tiles workgroups (a few VGPRs, so
+// LDS is the only limit) the runtime fits per CU with `dyn` bytes of dynamic
+// LDS each.
+extern "C" int copy_probe_lds_per_cu(void) {
+  int v = -1, dev = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
+  return v;
+}
+
+extern "C" int copy_probe_blocks_per_cu(unsigned long long dyn) {
+  int n = -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(copy_tiles), kBlock,
+                                                   static_cast<size_t>(dyn)) != hipSuccess)
+    return -1;
+  return n;
+}

@@ -310,6 +310,9 @@ for s in $STEPS; do
                         done
                 done
                 ;;
+        ldsinfo)
+                run lds_info 60 python3 -c "import torch, ctypes; torch.zeros(1, device='cuda'); l = ctypes.CDLL('tools/libcopy_probe.so'); print('lds_per_cu', l.copy_probe_lds_per_cu()); [print('dyn', d, 'blocks_per_cu', l.copy_probe_blocks_per_cu(ctypes.c_ulonglong(d))) for d in (0, 16384, 22528, 27136, 32768, 40960, 65536)]"
+                ;;
         grid)
                 # grid-stride launches of at most n workgroups (ISAL_HIP_GRID_CAP)
                 for r in 1 2; do
