@@ -67,8 +67,8 @@ def parse_args(argv=None):
                     help="e2e: distinct pinned host stripes cycled through (0 = max(2*depth, 4))")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="host threads / pinned processes for the CPU baselines; 0 = min(16, this "
-                         "process's CPUs) — 16 is the GPU box's CPU share per GPU")
+                    help="host threads / pinned processes for the CPU baselines; 0 = one per physical "
+                         "core of this process's affinity set (SURVEY.md §8(d))")
     ap.add_argument("--cold-ring", type=int, default=8,
                     help="distinct stripes each thread of the cold-cache SIMD-port baseline cycles over")
     ap.add_argument("--total-stripes", type=int, default=0,
@@ -552,12 +552,20 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=Fa
 
     counts = [0] * threads
     rng = np.random.default_rng(1)
-    # ring > 1: each thread cycles over `ring` distinct stripes (cold caches)
-    bufs = [[([rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)],
-              [np.zeros(n, np.uint8) for _ in range(p)]) for _ in range(ring)] for _ in range(threads)]
+    # ring > 1: each thread cycles over `ring` distinct stripes (cold caches);
+    # one random stripe copied into every buffer (distinct memory, same bytes)
+    proto = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    bufs = [[([x.copy() for x in proto], [np.zeros(n, np.uint8) for _ in range(p)]) for _ in range(ring)]
+            for _ in range(threads)]
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import cpu_ref_baseline as crb
+
+    cpus = crb.physical_cpus(threads)  # one thread pinned per physical core
     deadline = time.perf_counter() + seconds
 
     def worker(i):
+        if i < len(cpus):
+            os.sched_setaffinity(0, {cpus[i]})  # pid 0 = this thread
         srcs = [ptrs(b[0]) for b in bufs[i]]
         dsts = [ptrs(b[1]) for b in bufs[i]]
         t = tbls.ctypes.data_as(u8p)
@@ -587,7 +595,7 @@ def cpu_baseline(k, p, n, seconds, threads, check=None, impl="reference", crc=Fa
         "cores": threads,
         "kind": kind,
         "sample": f"{stripes} stripes of k={k} p={p} x {n} B, {what}, "
-                  f"{threads} threads x {wall:.1f} s"
+                  f"{threads} threads x {wall:.1f} s ({min(threads, len(cpus))} pinned one per physical core)"
                   + (f", each thread cycling over {ring} distinct stripes (cold caches)" if ring > 1
                      else ", each thread re-encoding one cache-warm stripe"),
         "parity_stripe_match": parity_ok,
@@ -616,7 +624,7 @@ def ref_harness_baseline(workload, k, p, n, procs):
         conv = f", converted from its (p+1)*len to this bench's (1+2p)*len bytes per call"
     else:
         return None
-    one, many = crb.run(which, 1), crb.run(which, procs)
+    one, many = crb.run(which, 1), crb.run(which, procs or 0)
     if "error" in one or "error" in many or phase not in many or phase not in one:
         return {"error": one.get("error") or many.get("error") or "phase missing"}
     host = crb.host_info()
@@ -631,12 +639,9 @@ def ref_harness_baseline(workload, k, p, n, procs):
                   f"(BENCHMARK_TIME), MB/s summed{conv}; reference ec_base.c path (no nasm: the "
                   f"AVX-512/GFNI kernels cannot be assembled)",
         "single_core_gib_s": gib(per_core),
-        "host": {a: host.get(a) for a in ("model", "sockets", "physical_cores", "cpus", "isa", "nasm")},
+        "host": {a: host.get(a) for a in ("model", "sockets", "physical_cores", "affinity_physical_cores",
+                                          "cgroup_cpu_quota", "cpus", "isa", "nasm")},
     }
-    if host.get("physical_cores"):
-        # the box grants this job a 16-CPU share of the host; the whole host
-        # would give at most per-core x physical cores
-        res["all_physical_cores_est_gib_s"] = round(res["single_core_gib_s"] * host["physical_cores"], 2)
     return res
 
 
@@ -1183,7 +1188,12 @@ def main(argv=None):
         result["roofline"]["frac_of_copy_ceiling"] = round(achieved / cc["gb_s"], 4)
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import cpu_ref_baseline as crb
+
+        # one pinned process (or thread) per physical core
+        # this process may use; the count is recorded in each baseline
+        threads = args.cpu_threads or len(crb.physical_cpus())
         if args.workload in ("encode", "decode", "update"):
             # the reference's own perf harness (erasure_code_perf.c /
             # erasure_code_update_perf.c) on this host's cores

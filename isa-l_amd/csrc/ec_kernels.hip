@@ -502,12 +502,19 @@ unsigned stripes_per_launch(int len, bool vec16) {
 
 }  // namespace
 
+// The 0/1 masks of a call, or none under ISAL_HIP_ENC_XOR=0 (read at launch,
+// so handles created before isal_hip_config_reload() follow it too).
+static const isal_hip_encmask* enc_xor_masks(const isal_hip_encmask* em) {
+  return isal_hip_knob(ISAL_HIP_KNOB_ENC_XOR) == 0 ? nullptr : em;
+}
+
 extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, int src_idx0,
                                       int dst_idx0, const uint32_t* d_tbl, int len, int k, int rows,
                                       long long nstripes, int vec16, const isal_hip_encmask* em,
                                       void* stream) {
   if (len <= 0 || rows <= 0 || nstripes <= 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  em = enc_xor_masks(em);
   const unsigned per = stripes_per_launch(len, vec16 != 0);
   for (long long s0 = 0; s0 < nstripes; s0 += per) {
     const unsigned ns = static_cast<unsigned>(nstripes - s0 < per ? nstripes - s0 : per);
@@ -568,6 +575,7 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int 
     return static_cast<int>(hipGetLastError());
   }
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + kTile - 1) / kTile);
+  em = enc_xor_masks(em);
   const bool x = em && (em->ok & 1u);
   const unsigned long long r0m = x ? em->r0[0] : 0ull;
   const unsigned c0m = x ? em->c0[0] : 0u;

@@ -256,7 +256,10 @@ isal_hip_enc_masks(int k, int rows, const unsigned char *gftbls, isal_hip_encmas
 {
         int g, l, j;
         memset(m, 0, sizeof(*m));
-        if (k < 1 || k > 64 || rows < 1 || isal_hip_knob(ISAL_HIP_KNOB_ENC_XOR) == 0)
+        /* computed whatever ISAL_HIP_ENC_XOR says: the launch applies the knob
+         * (ec_kernels.hip enc_xor_masks), so long-lived batch and pipeline
+         * handles follow isal_hip_config_reload() like the drop-in calls */
+        if (k < 1 || k > 64 || rows < 1)
                 return;
         for (g = 0; g * EC_MAX_ROWS_PER_PASS < rows && g < EC_MAX_PASSES; g++) {
                 const int r0 = g * EC_MAX_ROWS_PER_PASS;

@@ -368,12 +368,15 @@ ctx_tables(ctx_t *c, int k, int rows, const unsigned char *gftbls, const isal_hi
                         c->tcoef = x;
                         c->tcap_coef = n;
                 }
-                if (nd > c->tcap_tbl) {
-                        uint32_t *x = (uint32_t *) realloc(c->ttbl, nd * 4);
+                /* k = 0 (the empty sum: zero parity) has no tables at all; keep
+                 * one dword so that only a failed allocation returns NULL */
+                if (nd > c->tcap_tbl || !c->ttbl) {
+                        const size_t cap = nd ? nd : 1;
+                        uint32_t *x = (uint32_t *) realloc(c->ttbl, cap * 4);
                         if (!x)
                                 return NULL;
                         c->ttbl = x;
-                        c->tcap_tbl = nd;
+                        c->tcap_tbl = cap;
                 }
                 c->tk = -1; /* not valid until rebuilt */
                 for (i = 0; i < n; i++)

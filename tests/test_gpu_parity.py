@@ -1990,3 +1990,33 @@ def test_multi_device_encode_host_stripes_vs_oracle(engine, oracle, gpu):
     m.close()
     with pytest.raises(RuntimeError):
         engine.Multi(n, k, p, tbls, ndev=torch.cuda.device_count() + 1)
+
+
+@pytest.mark.parametrize("backend", ["gpu", "auto"])
+def test_k0_empty_sum_on_a_fresh_thread(engine, gpu, monkeypatch, backend):
+    """k = 0 is the empty sum: every parity row becomes zero (ec_base.c:309-325
+    with no sources). Run as a thread's FIRST GPU-route call, on device parity:
+    the per-thread table cache starts empty there and k * rows = 0 tables must
+    still be a valid (non-NULL) table."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_BACKEND", backend)
+    rows, n = 3, 4096 + 16
+    out = {}
+
+    def call():
+        try:
+            par = [torch.full((n,), 0x5A, dtype=torch.uint8, device=gpu) for _ in range(rows)]
+            engine.ec_encode_data(n, 0, rows, np.zeros(32, np.uint8), [], par)
+            torch.cuda.synchronize()
+            out["par"] = [_host(p) for p in par]
+        except BaseException as e:  # noqa: BLE001 - surfaced below
+            out["err"] = e
+
+    launches, fb = engine.kernel_launches(), engine.fallbacks()
+    t = threading.Thread(target=call)
+    t.start()
+    t.join()
+    assert "err" not in out, out.get("err")
+    assert all(not p.any() for p in out["par"])
+    assert engine.kernel_launches() > launches and engine.fallbacks() == fb

@@ -49,7 +49,8 @@ HARNESS = {
 
 def host_info() -> dict:
     """CPU model and core counts of this host (lscpu), plus this process's affinity."""
-    info = {"affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    info = {"affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+            "affinity_physical_cores": len(_physical_cpus(0)), "cgroup_cpu_quota": cgroup_cpu_quota()}
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
         kv = {}
@@ -76,8 +77,34 @@ def host_info() -> dict:
     return info
 
 
+def cgroup_cpu_quota() -> float | None:
+    """CPUs' worth of time this process's cgroup may use (cgroup v2 cpu.max,
+    v1 cfs quota/period), None when unlimited or unknown: a quota below the
+    core count caps what any number of pinned processes can measure."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
+def physical_cpus(n: int = 0) -> list[int]:
+    """n (0 = all) CPUs of this process's affinity set, one per physical core
+    where the topology says which logical CPUs are hyperthread siblings."""
+    return _physical_cpus(n)
+
+
 def _physical_cpus(n: int) -> list[int]:
-    """n CPUs of this process's affinity set, one per physical core where the
+    """n (0 = all) CPUs of this process's affinity set, one per physical core where the
     topology says which logical CPUs are hyperthread siblings."""
     cpus = sorted(os.sched_getaffinity(0))
     chosen, seen = [], set()
@@ -96,9 +123,10 @@ def _physical_cpus(n: int) -> list[int]:
     return chosen
 
 
-def run(which: str, procs: int, timeout: float = 120.0) -> dict:
-    """Run `procs` pinned copies of the harness at once (plus nothing else) and
-    sum their per-phase MB/s. Returns {phase: {"mb_s_sum", "mb_s_per_proc"}, ...}."""
+def run(which: str, procs: int, timeout: float = 180.0) -> dict:
+    """Run `procs` (0 = one per physical core of this process's affinity set)
+    pinned copies of the harness at once (plus nothing else) and sum their
+    per-phase MB/s. Returns {phase: {"mb_s_sum", "mb_s_per_proc"}, ...}."""
     argv, names = HARNESS[which]
     exe = os.path.join(REF, argv[0])
     if not os.path.exists(exe):
@@ -133,11 +161,12 @@ def run(which: str, procs: int, timeout: float = 120.0) -> dict:
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--procs", type=int, default=0, help="0 = 1 and min(16, affinity)")
+    ap.add_argument("--procs", type=int, default=-1,
+                    help="-1 = 1 and one per physical core of the affinity set; 0 = the latter only")
     ap.add_argument("--which", choices=sorted(HARNESS), default="encode")
     a = ap.parse_args(argv)
     out = {"host": host_info()}
-    counts = [a.procs] if a.procs else sorted({1, min(16, len(os.sched_getaffinity(0)))})
+    counts = [a.procs] if a.procs >= 0 else [1, 0]
     for n in counts:
         out[f"procs_{n}"] = run(a.which, n)
     print(json.dumps(out, indent=1))

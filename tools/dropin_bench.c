@@ -42,10 +42,17 @@ typedef struct {
         int t, nthreads, k, p, len, stripes;
         long long fixed_calls;
         unsigned char *base, *tbls;
-        double deadline;
         long long calls;
         double first_call_us;
 } worker_t;
+
+/* Warm-up and timed calls run on the SAME threads: the library's per-thread
+ * context (stream, pinned argument buffer, cached tables) lives as long as its
+ * thread, so a thread created for the timed run would pay its context
+ * creation inside the timed window. */
+static pthread_barrier_t warm_done, go;
+static double g_deadline;
+#define WARM_CALLS 2
 
 static unsigned char *
 shard(const worker_t *w, int s, int i)
@@ -53,30 +60,41 @@ shard(const worker_t *w, int s, int i)
         return w->base + ((size_t) s * (size_t) (w->k + w->p) + (size_t) i) * (size_t) w->len;
 }
 
+static void
+encode_one(worker_t *w, int *s)
+{
+        unsigned char *data[256], *coding[256];
+        int i;
+        for (i = 0; i < w->k; i++)
+                data[i] = shard(w, *s, i);
+        for (i = 0; i < w->p; i++)
+                coding[i] = shard(w, *s, w->k + i);
+        ec_encode_data(w->len, w->k, w->p, w->tbls, data, coding);
+        *s += w->nthreads;
+        if (*s >= w->stripes)
+                *s = w->t % w->stripes;
+}
+
 static void *
 run(void *arg)
 {
         worker_t *w = (worker_t *) arg;
-        unsigned char *data[256], *coding[256];
         int s = w->t, i;
         (void) hipSetDevice(0);
+        for (i = 0; i < WARM_CALLS; i++)
+                encode_one(w, &s);
+        pthread_barrier_wait(&warm_done);
+        pthread_barrier_wait(&go); /* main has set g_deadline */
         w->calls = 0;
         for (;;) {
                 double t0;
-                if (w->fixed_calls ? w->calls >= w->fixed_calls : now() >= w->deadline)
+                if (w->fixed_calls ? w->calls >= w->fixed_calls : now() >= g_deadline)
                         break;
-                for (i = 0; i < w->k; i++)
-                        data[i] = shard(w, s, i);
-                for (i = 0; i < w->p; i++)
-                        coding[i] = shard(w, s, w->k + i);
                 t0 = w->calls ? 0 : now();
-                ec_encode_data(w->len, w->k, w->p, w->tbls, data, coding);
+                encode_one(w, &s);
                 if (!w->calls)
                         w->first_call_us = (now() - t0) * 1e6;
                 w->calls++;
-                s += w->nthreads;
-                if (s >= w->stripes)
-                        s = w->t % w->stripes;
         }
         return NULL;
 }
@@ -190,19 +208,14 @@ main(int argc, char **argv)
                 w[i] = (worker_t){.t = i, .nthreads = nthreads, .k = k, .p = p, .len = len,
                                   .stripes = stripes, .fixed_calls = fixed, .base = base, .tbls = tbls};
         }
-        /* warm every thread's context (stream, argument buffers) first */
-        for (i = 0; i < nthreads; i++) {
-                w[i].fixed_calls = 2;
-                pthread_create(&th[i], NULL, run, &w[i]);
-        }
+        pthread_barrier_init(&warm_done, NULL, (unsigned) nthreads + 1);
+        pthread_barrier_init(&go, NULL, (unsigned) nthreads + 1);
         for (i = 0; i < nthreads; i++)
-                pthread_join(th[i], NULL);
-        t0 = now();
-        for (i = 0; i < nthreads; i++) {
-                w[i].fixed_calls = fixed;
-                w[i].deadline = t0 + seconds;
                 pthread_create(&th[i], NULL, run, &w[i]);
-        }
+        pthread_barrier_wait(&warm_done); /* every thread's context is warm */
+        t0 = now();
+        g_deadline = t0 + seconds;
+        pthread_barrier_wait(&go);
         for (i = 0; i < nthreads; i++) {
                 pthread_join(th[i], NULL);
                 calls += w[i].calls;
