@@ -59,9 +59,11 @@ def parse_args(argv=None):
     ap.add_argument("--len", type=int, default=1 << 20, help="shard bytes")
     ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU per step")
     ap.add_argument("--workload", choices=["encode", "decode", "update", "encode-crc", "crc", "crc64", "encode-crc64",
-                                           "e2e-update", "e2e-encode", "c1", "dropin"],
+                                           "e2e-update", "e2e-encode", "c1", "dropin", "pq_gen", "xor_gen",
+                                           "pq_check"],
                     default="encode",
-                    help="e2e-*: host-resident (pinned) stripes streamed through the pipeline")
+                    help="e2e-*: host-resident (pinned) stripes streamed through the pipeline; pq_gen / "
+                         "xor_gen / pq_check: RAID-6 / RAID-5 parity over --k sources (raid.h; p is 2 / 1)")
     ap.add_argument("--depth", type=int, default=3, help="e2e pipeline depth (stripes in flight)")
     ap.add_argument("--ring", type=int, default=0,
                     help="e2e: distinct pinned host stripes cycled through (0 = max(2*depth, 4))")
@@ -85,6 +87,8 @@ def parse_args(argv=None):
     ap.add_argument("--dropin-threads", default="1,4,16",
                     help="dropin: calling threads per run (tools/dropin_bench), comma-separated")
     ap.add_argument("--dropin-seconds", type=float, default=3.0, help="dropin: seconds per thread count")
+    ap.add_argument("--dropin-op", default="encode", choices=["encode", "pq_gen", "xor_gen", "pq_check", "xor_check"],
+                    help="dropin: the synchronous call driven per stripe (ec_encode_data or a raid.h call)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the distributed harness without a GPU (gloo, dummy step)")
     return ap.parse_args(argv)
@@ -335,6 +339,90 @@ SELF_CHECK_METHOD.update({
     "decode": "every recovered shard of every stripe == the erased original",
     "crc": "checksum-only CRC32C == the fused kernel's",
     "crc64": "crc(P0) == XOR of the sources' CRC64 (linearity) on 3 stripes"})
+
+
+SELF_CHECK_METHOD.update({
+    "pq_gen": "3 stripes: P == XOR of the sources, Q == sum of 2^j * D_j (host gf_mul of the sources' bytes "
+              "at 4096 sampled columns), and the batch verify finds every stripe consistent",
+    "xor_gen": "3 stripes: P == XOR of the sources, and the batch verify finds every stripe consistent",
+    "pq_check": "every stripe consistent after the timed checks; then one byte flipped in a source of one stripe "
+                "and in Q of another: exactly those two stripes flagged, at the flipped column (row 0 for a "
+                "source byte, row 1 for Q)"})
+
+# raid.h workloads: parity rows
+RAID_ROWS = {"pq_gen": 2, "xor_gen": 1, "pq_check": 2}
+
+
+def raid_coef(k: int, p: int):
+    """Coefficient rows of RAID P (all ones) and Q (2^j for source j): the
+    matrix pq_gen / xor_gen compute (raid_base.c:44-68,100-118)."""
+    import numpy as np
+
+    import isal_amd
+
+    c = np.ones((p, k), np.uint8)
+    if p == 2:
+        q = 1
+        for j in range(k):
+            c[1, j] = q
+            q = isal_amd.gf_mul(q, 2)
+    return c.reshape(-1)
+
+
+def verify_kernel(rows: int, k: int, coef) -> str:
+    """The batch verify kernel the library launches (ec_kernels.hip
+    isal_hip_launch_verify_batch: load group verify_group(k), tile order with
+    the XCD mapping of a batch, bit 0 = the 0/1 XOR path)."""
+    import numpy as np
+
+    c = np.asarray(coef, dtype=np.uint8).reshape(rows, k)
+    fl = 1 if (os.environ.get("ISAL_HIP_ENC_XOR") != "0" and k <= 64 and int(c[0].max()) <= 1
+               and int(c[:, 0].max()) <= 1) else 0
+    u = next((g for g in (10, 8, 6, 4) if k >= g and k % g == 0), 4)
+    return f"ec_verify_v16<{rows}, EncPol<{u}, 2, 2, 0>, {fl}>"
+
+
+def raid_self_check(workload, batch, data, out, k, p, n, S, h, dev) -> bool:
+    """No oracle: P and Q recomputed on the host from the sources' bytes at
+    sampled columns with the library's gf_mul (itself pinned by the reference
+    fixtures), and the engine's batch verify as a second opinion (pq_check: it
+    must also localise injected corruption)."""
+    import numpy as np
+    import torch
+
+    import isal_amd
+
+    ok = True
+    bad = torch.empty(S, dtype=torch.int64, device=dev)
+    batch.check(bad, h)
+    torch.cuda.synchronize(dev)
+    ok &= bool((bad == -1).all())
+    cols = np.unique(np.concatenate([np.arange(64), np.arange(n - 64, n),
+                                     np.random.default_rng(3).integers(0, n, 4096)]))
+    mul = np.array([[isal_amd.gf_mul(a, b) for b in range(256)] for a in range(256)], np.uint8)
+    tcols = torch.as_tensor(cols, device=dev)
+    for s_ in sorted({0, S // 2, S - 1}):
+        src = data[s_][:, tcols].cpu().numpy()
+        par = out[s_][:, tcols].cpu().numpy()
+        ok &= bool(np.array_equal(np.bitwise_xor.reduce(src, axis=0), par[0]))
+        if p == 2:
+            q, g = np.zeros(len(cols), np.uint8), 1
+            for j in range(k):
+                q ^= mul[g][src[j]]
+                g = isal_amd.gf_mul(g, 2)
+            ok &= bool(np.array_equal(q, par[1]))
+    if workload == "pq_check" and S >= 2:
+        s1, s2, c1, c2 = 0, S - 1, n // 3, n - 5
+        data[s1, 3, c1] ^= 0x10
+        out[s2, 1, c2] ^= 0x01
+        batch.check(bad, h)
+        torch.cuda.synchronize(dev)
+        want = torch.full((S,), -1, dtype=torch.int64, device=dev)
+        want[s1], want[s2] = c1 << 8, (c2 << 8) | 1
+        ok &= bool(torch.equal(bad, want))
+        data[s1, 3, c1] ^= 0x10
+        out[s2, 1, c2] ^= 0x01
+    return ok
 
 
 def erasure_set(k: int, p: int, s: int) -> list[int]:
@@ -901,6 +989,8 @@ def main(argv=None):
     torch.cuda.set_device(d.gpu)
     dev = torch.device("cuda", d.gpu)
     k, p, n, S = args.k, args.p, args.len, args.stripes
+    if args.workload in RAID_ROWS:
+        p = RAID_ROWS[args.workload]
     a = np.frombuffer(control_plane_matrix(d, k, p), dtype=np.uint8)
     if args.workload.startswith("e2e"):
         return e2e(args, d, a, k, p, n)
@@ -1023,6 +1113,23 @@ def main(argv=None):
                 kernel = f"crc64_shards_pre<{b8}, {pp}>"
             workload = (f"CRC64 (crc64_ecma_refl) of all k+p={k + p} shards, {n} B x {S} "
                         f"stripes/GPU, device-resident")
+        elif args.workload in RAID_ROWS:
+            # RAID-6 P+Q / RAID-5 P over k sources (raid.h pq_gen / xor_gen /
+            # pq_check; raid_base.c:44-140): the encode kernels with rows {1,..,1}
+            # and {2^0, 2^1, ..} (the Horner loop q = D_j ^ 2q is sum 2^j D_j),
+            # the verify kernel for the check. Bytes: (k+p)*len per stripe, the
+            # reference harness's (sources+2)*len (raid/pq_gen_perf.c:79)
+            coef = raid_coef(k, p)
+            batch.set_tables(isal_amd.ec_init_tables(k, p, coef))
+            bytes_per_launch = (k + p) * n * S
+            if args.workload == "pq_check":
+                batch.encode(torch.cuda.current_stream(dev).cuda_stream)
+                bad = torch.empty(S, dtype=torch.int64, device=dev)
+                kernel = verify_kernel(p, k, coef)
+            else:
+                kernel = enc_kernel(p, k, coef)
+            workload = (f"{args.workload}: RAID-{5 if p == 1 else 6} parity over {k} sources "
+                        f"({'P' if p == 1 else 'P+Q'}), {n} B shards x {S} stripes/GPU, device-resident")
         else:
             bytes_per_launch = (1 + 2 * p) * n * S
             kernel = f"ec_update_v16<{p}>"
@@ -1045,6 +1152,8 @@ def main(argv=None):
             batch.crc64(0, 0, crc_out, h)
         elif args.workload == "encode-crc64":
             batch.encode_crc64(0, 0, crc_out, h)
+        elif args.workload == "pq_check":
+            batch.check(bad, h)
         else:
             batch.encode(h)
 
@@ -1113,6 +1222,8 @@ def main(argv=None):
     elif args.workload == "decode":
         for i, e in enumerate(errs):
             ok &= bool(torch.equal(out[:, i], data[:, e]))
+    elif args.workload in RAID_ROWS:
+        ok &= raid_self_check(args.workload, batch, data, out, k, p, n, S, h, dev)
     self_check = None if args.workload == "update" else bool(d.max(0.0 if ok else 1.0) == 0.0)
     digest = None
     if args.workload in ("encode", "decode"):
@@ -1321,17 +1432,22 @@ def dropin(args):
     if not os.path.exists(exe):
         raise SystemExit("bench.py: tools/dropin_bench not built (make -C isa-l_amd tools)")
     k, p, n = args.k, args.p, args.len
+    op = args.dropin_op
+    if op != "encode":
+        p = 2 if op.startswith("pq") else 1
     stripes = min(args.stripes, 64)
     runs = []
     for t in [int(x) for x in args.dropin_threads.split(",") if x]:
-        r = subprocess.run([exe, str(k), str(p), str(n), str(stripes), str(t), str(args.dropin_seconds)],
+        r = subprocess.run([exe, str(k), str(p), str(n), str(stripes), str(t), str(args.dropin_seconds), "0",
+                            args.dropin_op],
                            capture_output=True, text=True, timeout=120 + 2 * args.dropin_seconds)
         if r.returncode != 0:
             raise SystemExit(f"bench.py: dropin_bench failed ({r.returncode}): {r.stderr[-2000:]}")
         runs.append(json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1]))
     top = runs[-1]
     result = {
-        "metric": "ec_encode_data drop-in GiB/s device-resident, one synchronous call per stripe",
+        "metric": (f"{'ec_encode_data' if op == 'encode' else op} drop-in GiB/s device-resident, one synchronous "
+                   "call per stripe"),
         "value": round(top["gib_s"], 2),
         "unit": "GiB/s",
         "n_gpus": 1,
@@ -1343,8 +1459,10 @@ def dropin(args):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (xorshift bytes copied into HBM; 64 resident stripes cycled)",
-        "config": {"workload": f"drop-in ec_encode_data(len={n}, k={k}, rows={p}) per stripe on hipMalloc'ed "
-                               f"shards, {stripes} stripes, from {top['threads']} host threads",
+        "config": {"workload": (f"drop-in ec_encode_data(len={n}, k={k}, rows={p})" if op == "encode" else
+                                f"drop-in {op}(vects={k + p}, len={n})") +
+                               f" per stripe on hipMalloc'ed shards, {stripes} stripes, from {top['threads']} "
+                               "host threads",
                    "k": k, "p": p, "shard_bytes": n},
         "threads": [{a: r[a] for a in ("threads", "calls", "us_per_call", "calls_per_s", "gib_s", "self_check")}
                     for r in runs],

@@ -54,6 +54,14 @@ int isal_hip_batch_encode(isal_hip_batch *b, void *stream);
  * data[s*k + vec_i] is folded into coding[s*rows + l] for all l. */
 int isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream);
 
+/* Enqueue a verify of every stripe (the xor_check / pq_check question for a
+ * whole batch, e.g. a scrub): each stripe's coding rows are recomputed from
+ * its sources and compared with the stored bytes; nothing is written to the
+ * shards. bad: DEVICE array of nstripes words, bad[s] = ~0 when stripe s is
+ * consistent, else its first mismatch as column << 8 | row (smallest column,
+ * then row). Needs every shard 16-byte aligned (ISAL_HIP_EINVAL otherwise). */
+int isal_hip_batch_check(isal_hip_batch *b, unsigned long long *bad, void *stream);
+
 int isal_hip_batch_destroy(isal_hip_batch *b);
 
 /*

@@ -278,6 +278,8 @@ __device__ __forceinline__ void have_coefs(const Coef (&c)[P]) {
 //   kEncLds  (a bit, with either) the low table halves from an LDS copy
 //            (low_halves), the rest from SGPRs.
 enum : int { kEncLUT = 0, kEncXor = 1, kEncLds = 2 };
+// Launch-bounds flag of the verify kernels (they also hold the stored parity).
+constexpr int kEncVerify = 16;
 
 // Source pairs share XOR3s but hold two sources' tables in SGPRs (5 dwords per
 // looked-up row each): pairs while at most 4 rows per source are looked up
@@ -405,7 +407,7 @@ __device__ __forceinline__ void dot_bytes(const uint64_t* __restrict__ sp, int s
 // is not always better: the scheduler then spends it and may spill).
 template <int P, int U, int FL = 0>
 constexpr int enc_waves() {
-  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8 + ((FL & 1) ? 8 : 0) + (FL == 16 ? 16 : 0) +
+  constexpr int est = (4 * U + 4 * P + 32 + 7) / 8 * 8 + ((FL & 1) ? 8 : 0) + ((FL & 16) ? 16 : 0) +
                       (P >= 5 && U <= 6 ? (P == 8 && U == 4 ? 32 : 16) : 0);
   constexpr int w = 512 / (est + ((FL & kEncLds) ? 16 : 0));
   // kEncLds pairs every pass: two sources' low halves of every row in VGPRs;

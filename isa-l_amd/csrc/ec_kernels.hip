@@ -27,6 +27,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <type_traits>
+#include <utility>
+
 
 #include "ec_device.h"
 
@@ -93,18 +96,241 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encod
   encode_items<P, Pol, FL>(ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
 }
 
+// End of a kernel-argument call (isal_hip_kdone): the calling
+// thread spins on a page-locked host word instead of waiting for the
+// runtime's completion signal and its wake-up (~9 us of the call,
+// profiles/r04_dropin_hiptrace_b.txt). The kernel-argument kernels store
+// their 16- and 4-byte outputs with sc1 (write-through past the XCD's L2), so
+// a workgroup publishes them at agent scope — to every XCD, to copies and to
+// later kernels on any stream — by waiting for them (vmcnt) before it counts
+// itself; only the workgroup that ran the per-byte tail (plain byte stores,
+// `tail`) also issues an agent-scope release (an L2 writeback: once per call,
+// not once per workgroup). The last workgroup to count resets the counter
+// (and a verify's result word) for the thread's next call — the next launch
+// on the same stream cannot start before this one ends — and writes the
+// result, then the call's sequence number, to the host mailbox. All plain
+// vector memory operations.
+__device__ __forceinline__ void karg_done(const isal_hip_kdone& d, bool tail) {
+  if (d.cnt == nullptr) return;  // wave-uniform: the caller synchronises the stream
+  if (tail) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned n = gridDim.x, b = blockIdx.x;
+    const unsigned gsz = max(32u, (n + ISAL_HIP_KDONE_GROUPS - 1) / ISAL_HIP_KDONE_GROUPS);
+    const unsigned g = b / gsz, gn = min(gsz, n - g * gsz), ng = (n + gsz - 1) / gsz;
+    unsigned* gc = d.cnt + g * ISAL_HIP_KDONE_STRIDE;
+    unsigned* top = d.cnt + ISAL_HIP_KDONE_GROUPS * ISAL_HIP_KDONE_STRIDE;
+    if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gn - 1) return;
+    __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
+      __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long r = ~0ull;
+      if (d.res != nullptr) {
+        r = __hip_atomic_load(d.res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d.res, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(d.mail + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the result lands before the sequence number
+      __hip_atomic_store(d.mail, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // One stripe whose shard pointers and coefficient tables travel as kernel
 // arguments (isal_hip_karg, 2 KiB): the synchronous drop-in call on
 // device-resident shards launches this with no argument upload before it
 // (a hipMemcpyAsync + blit kernel per call otherwise).
 template <int P, class Pol, int FL>
 __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encode_karg(
-    const isal_hip_karg a, int len, int k, unsigned tiles, unsigned long long r0m, unsigned c0m) {
+    const isal_hip_karg a, const isal_hip_kdone d, int len, int k, unsigned tiles, unsigned long long r0m,
+    unsigned c0m) {
   // `a` is the first argument, at offset 0 of the kernarg segment: read it in
   // place (scalar loads) — indexing the by-value copy with runtime indices
   // made the compiler copy all 2 KiB of it to scratch.
   const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
   encode_items<P, Pol, FL>(ka->ptrs, k + P, 0, k, ka->tbl, len, k, tiles, tiles, r0m, c0m);
+  karg_done(d, (len & (kVec - 1)) != 0 && blockIdx.x == gridDim.x - 1);
+}
+
+// ---------------------------------------------------------------------------
+// Wide passes with the sources staged through LDS by LDS-DMA (ENC_GLDS)
+//
+// The register-staged encode loads a group of U sources, folds it, loads the
+// next: between groups a wave has no load in flight, and with 6-8 rows the
+// fold is long (k20p6: four dependent groups of 5 per tile at 3-4 waves per
+// SIMD). Here each wave owns a ring of R 1-KiB LDS slots (64 lanes
+// x 16 B, the lane-linear layout one global_load_lds_dwordx4 writes) and keeps
+// R source loads in flight all the time: it waits for source j's DMA with a
+// counted vmcnt (nothing else orders a ds_read behind the issuing wave's own
+// LDS-DMA), reads the slot with ds_read_b128, refills the slot with source
+// j + R and folds j — the loads cost no VGPRs. The DMA and the slot reads are
+// inline asm, so hipcc neither counts nor waits for them: every wait here is
+// explicit. Tiles that are not full (a shard's ragged end) take the
+// register path.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+template <class F, int... I>
+__device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const lds_u8*)p));
+}
+
+// 16 bytes per lane from base + voff into LDS at m0 + 16 * lane (nt)
+__device__ __forceinline__ void glds16(uint64_t base_, uint32_t voff, uint32_t m0) {
+  // readfirstlane returns a (signed) int: widen each half through uint32_t,
+  // or a low half with bit 31 set sign-extends over the high half
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base_ >> 32)));
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base_)));
+  const uint64_t base = (static_cast<uint64_t>(hi) << 32) | lo;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(base), "s"(m0)
+               : "memory");
+}
+
+template <int OA, int OB>
+__device__ __forceinline__ void lds_read2(uint4& a, uint4& b, uint32_t addr) {
+  u32x4 x, y;
+  asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(x), "=&v"(y)
+               : "v"(addr), "i"(OA), "i"(OB)
+               : "memory");
+  a = make_uint4(x.x, x.y, x.z, x.w);
+  b = make_uint4(y.x, y.y, y.z, y.w);
+}
+
+template <int OA>
+__device__ __forceinline__ void lds_read1(uint4& a, uint32_t addr) {
+  u32x4 x;
+  asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=&v"(x) : "v"(addr), "i"(OA) : "memory");
+  a = make_uint4(x.x, x.y, x.z, x.w);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// vmcnt(n) for a wave-uniform runtime n < 8
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  switch (n) {
+    case 0: vm_wait<0>(); break;
+    case 1: vm_wait<1>(); break;
+    case 2: vm_wait<2>(); break;
+    case 3: vm_wait<3>(); break;
+    case 4: vm_wait<4>(); break;
+    case 5: vm_wait<5>(); break;
+    case 6: vm_wait<6>(); break;
+    default: vm_wait<7>(); break;
+  }
+}
+
+template <int P, int R, int FL>
+__global__ __launch_bounds__(kBlock, 4) void ec_encode_glds(const uint64_t* __restrict__ ptrs, int ptr_stride,
+                                                           int src0, int dst0, const uint32_t* __restrict__ tbl,
+                                                           int len, int k, unsigned nitems, unsigned tiles,
+                                                           unsigned long long r0m, unsigned c0m) {
+  static_assert(R % 2 == 0 && R >= 4 && R <= 8, "ring of 4..8 slots, folded in pairs");
+  constexpr bool X = (FL & kEncXor) != 0;
+  constexpr bool LT = (FL & kEncLds) != 0;
+  static_assert(LT || P - (X ? 1 : 0) <= 4, "pairs from SGPR tables only up to 4 looked-up rows");
+  extern __shared__ uint2 enc_lt[];
+  const int ltn = LT ? k * P : 0;
+  if constexpr (LT) {
+    for (int i = threadIdx.x; i < ltn; i += kBlock) enc_lt[i] = make_uint2(tbl[i * kTbl], tbl[i * kTbl + 2]);
+  }
+  __syncthreads();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ring = lds_off(enc_lt) + ((static_cast<uint32_t>(ltn) * 8 + 1023) & ~1023u) + wave * (R * 1024);
+  const uint32_t mine = ring + (threadIdx.x & 63) * kVec;
+  const uint2* lt = enc_lt;
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned v = xcd_item(w, nitems, 1);
+    const unsigned stripe = v / tiles;
+    const unsigned tile = v - stripe * tiles;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
+    const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
+    if (static_cast<long long>(tile + 1) * kTile <= len) {
+      vm_wait<0>();  // this wave's stores of an earlier item (one counter for loads and stores)
+      const uint32_t voff = static_cast<uint32_t>(off);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (r < k) glds16(sp[src0 + r], voff, ring + r * 1024);
+      uint32_t acc[P][4];
+#pragma unroll
+      for (int l = 0; l < P; ++l) acc[l][0] = acc[l][1] = acc[l][2] = acc[l][3] = 0;
+      for (int j0 = 0; j0 < k; j0 += R) {
+        // slots r, r + 1 (compile-time LDS offsets): sources j0 + r, j0 + r + 1
+        auto step = [&](auto rc) {
+          constexpr int r = decltype(rc)::value * 2;
+          const int j = j0 + r;
+          if (j >= k) return;
+          uint4 x0, x1;
+          if (j + 1 < k) {
+            // loads issued: sources < min(k, j + R); wait for j + 1
+            if (j + R <= k)
+              vm_wait<R - 2>();
+            else
+              vm_wait_rt(k - 2 - j);
+            lds_read2<r * 1024, (r + 1) * 1024>(x0, x1, mine);
+            if (j + R < k) glds16(sp[src0 + j + R], voff, ring + r * 1024);
+            if (j + 1 + R < k) glds16(sp[src0 + j + 1 + R], voff, ring + (r + 1) * 1024);
+            __builtin_amdgcn_sched_barrier(0);
+            if (X && j == 0) {
+#pragma unroll
+              for (int l = 0; l < P; ++l) {
+                const uint32_t m = (c0m >> l) & 1u ? ~0u : 0u;
+                acc[l][0] = x0.x & m;
+                acc[l][1] = x0.y & m;
+                acc[l][2] = x0.z & m;
+                acc[l][3] = x0.w & m;
+              }
+              mac16<P, X, LT>(acc, x1, tbl + P * kTbl, r0_mask(r0m, 1), lt + P);
+            } else {
+              mac16x2<P, X, LT>(acc, x0, x1, tbl + j * P * kTbl, tbl + (j + 1) * P * kTbl,
+                                X ? r0_mask(r0m, j) : 0u, X ? r0_mask(r0m, j + 1) : 0u, lt + j * P,
+                                lt + (j + 1) * P);
+            }
+          } else {
+            vm_wait<0>();
+            lds_read1<r * 1024>(x0, mine);
+            __builtin_amdgcn_sched_barrier(0);
+            if (X && j == 0) {
+#pragma unroll
+              for (int l = 0; l < P; ++l) {
+                const uint32_t m = (c0m >> l) & 1u ? ~0u : 0u;
+                acc[l][0] = x0.x & m;
+                acc[l][1] = x0.y & m;
+                acc[l][2] = x0.z & m;
+                acc[l][3] = x0.w & m;
+              }
+            } else {
+              mac16<P, X, LT>(acc, x0, tbl + j * P * kTbl, X ? r0_mask(r0m, j) : 0u, lt + j * P);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        static_for(step, std::make_integer_sequence<int, R / 2>{});
+      }
+#pragma unroll
+      for (int l = 0; l < P; ++l)
+        store16<kBufNT>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
+    } else if (off + kVec <= len) {
+      uint32_t acc[P][4];
+      accum16<P, EncPol<4, kBufNT, kBufNT, 2>, FL>(acc, sp + src0, tbl, k, off, len, r0m, c0m, lt);
+#pragma unroll
+      for (int l = 0; l < P; ++l)
+        store16<kBufNT>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
+    } else if (off < len) {
+      dot_bytes<P>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off));
+    }
+  }
 }
 
 // Any alignment: one lane per byte column, 256 columns per work item.
@@ -123,26 +349,32 @@ __global__ __launch_bounds__(kBlock) void ec_encode_b1(const uint64_t* __restric
 }
 
 // ---------------------------------------------------------------------------
-// Verify (xor_check / pq_check): recompute the parity of each column and
-// compare it with the stored rows at dst; the first mismatching (column, row)
-// is reduced into *bad with atomicMin. Nothing is written to the shards.
+// Verify (xor_check / pq_check): recompute the parity of each column exactly
+// like the encode (same load groups, 0/1 XOR path) and compare it with the
+// stored rows at dst; mismatches lower *bad (key = column << 8 | row) with
+// atomicMin — an LDS word per workgroup (generic launch: one slot per
+// workgroup, so the result may live in page-locked host memory) or the
+// call's device result word (kernel-argument launch). Nothing is written to
+// the shards.
 // ---------------------------------------------------------------------------
-template <int P>
-__global__ __launch_bounds__(kBlock, (enc_waves<P, 4, 16>())) void ec_verify_v16(
-    const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
-    const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles,
-    unsigned long long* __restrict__ slots, int row0, long long col0) {
-  __shared__ unsigned long long blk_min;
-  if (threadIdx.x == 0) blk_min = ~0ull;
-  __syncthreads();
-  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+// sbad != nullptr (a batch): each stripe's mismatches lower sbad[stripe]
+// instead, and items run in the XCD-contiguous order of the encode.
+template <int P, class Pol, int FL>
+__device__ __forceinline__ void verify_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
+                                             const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems,
+                                             unsigned tiles, unsigned long long r0m, unsigned c0m,
+                                             unsigned long long* bad, int row0, long long col0,
+                                             unsigned long long* sbad = nullptr) {
+  for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
+    const unsigned w = xcd_item(ww, nitems, sbad != nullptr);
     const unsigned stripe = w / tiles;
+    if (sbad != nullptr) bad = sbad + stripe;
     const unsigned tile = w - stripe * tiles;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
       uint32_t acc[P][4];
-      accum16<P, EncNT<4>>(acc, sp + src0, tbl, k, off, len);
+      accum16<P, Pol, FL>(acc, sp + src0, tbl, k, off, len, r0m, c0m);
 #pragma unroll
       for (int l = 0; l < P; ++l) {
         const uint4 e = load16<kBufNT>(sp[dst0 + l], off, len);
@@ -150,17 +382,41 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, 4, 16>())) void ec_verify_v16
 #pragma unroll
         for (int d = 0; d < 4; ++d)
           if (x[d]) {
-            note_mismatch(&blk_min, col0 + off + 4 * d + (__builtin_ctz(x[d]) >> 3), row0 + l);
+            note_mismatch(bad, col0 + off + 4 * d + (__builtin_ctz(x[d]) >> 3), row0 + l);
             break;
           }
       }
     } else if (off < len) {
-      dot_bytes<P, true>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off), &blk_min, row0,
-                         col0);
+      dot_bytes<P, true>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off), bad, row0, col0);
     }
   }
+}
+
+template <int P, class Pol, int FL>
+__global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL | kEncVerify>())) void ec_verify_v16(
+    const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0, const uint32_t* __restrict__ tbl,
+    int len, int k, unsigned nitems, unsigned tiles, unsigned long long* __restrict__ slots, int row0,
+    long long col0, unsigned long long r0m, unsigned c0m, unsigned long long* sbad) {
+  __shared__ unsigned long long blk_min;
+  if (threadIdx.x == 0) blk_min = ~0ull;
   __syncthreads();
-  if (threadIdx.x == 0) slots[blockIdx.x] = blk_min;
+  verify_items<P, Pol, FL>(ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m, &blk_min, row0,
+                           col0, sbad);
+  if (slots != nullptr) {
+    __syncthreads();
+    if (threadIdx.x == 0) slots[blockIdx.x] = blk_min;
+  }
+}
+
+// One stripe's verify with its arguments in the kernarg segment (as
+// ec_encode_karg); the result travels through the completion mailbox.
+template <int P, class Pol, int FL>
+__global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL | kEncVerify>())) void ec_verify_karg(
+    const isal_hip_karg a, const isal_hip_kdone d, int len, int k, unsigned tiles, unsigned long long r0m,
+    unsigned c0m) {
+  const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
+  verify_items<P, Pol, FL>(ka->ptrs, k + P, 0, k, ka->tbl, len, k, tiles, tiles, r0m, c0m, d.res, 0, 0);
+  karg_done(d, false);
 }
 
 template <int P>
@@ -201,7 +457,7 @@ __device__ __forceinline__ void mad_bytes(const uint64_t* __restrict__ sp, int s
   }
 }
 
-template <int P>
+template <int P, int ST = kBufNT>
 __device__ __forceinline__ void update_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src_idx,
                                              int dst0, const uint32_t* __restrict__ tbl, int len,
                                              unsigned nitems, unsigned tiles, int xcd) {
@@ -224,7 +480,7 @@ __device__ __forceinline__ void update_items(const uint64_t* __restrict__ ptrs, 
         d[l].y ^= gf_mul4(c, s1);
         d[l].z ^= gf_mul4(c, s2);
         d[l].w ^= gf_mul4(c, s3);
-        store16<kBufNT>(sp[dst0 + l], off, d[l], len);
+        store16<ST>(sp[dst0 + l], off, d[l], len);
       }
     } else if (off < len) {
       mad_bytes<P>(sp, src_idx, dst0, tbl, off, static_cast<int>(len - off));
@@ -241,9 +497,10 @@ __device__ __forceinline__ uint32_t load4nt(uint64_t base, long long off, int le
   return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(off), 0, 2 /* nt */));
 }
 
-__device__ __forceinline__ void store4nt(uint64_t base, long long off, uint32_t v, int len) {
+// sc1 + nt (gfx950 CPol 0x12): write-through, see karg_done
+__device__ __forceinline__ void store4wt(uint64_t base, long long off, uint32_t v, int len) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, len, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(v), rs, static_cast<int>(off), 0, 2 /* nt */);
+  __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(v), rs, static_cast<int>(off), 0, 0x12);
 }
 
 template <int P>
@@ -254,7 +511,8 @@ __device__ __forceinline__ void fold4(uint32_t (&acc)[P], uint32_t x, const uint
 }
 
 template <int P>
-__global__ __launch_bounds__(kBlock) void ec_encode_karg4(const isal_hip_karg a, int len, int k) {
+__global__ __launch_bounds__(kBlock) void ec_encode_karg4(const isal_hip_karg a, const isal_hip_kdone d, int len,
+                                                          int k) {
   const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
   const long long off = (static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x) * 4;
   if (off + 4 <= len) {
@@ -271,10 +529,11 @@ __global__ __launch_bounds__(kBlock) void ec_encode_karg4(const isal_hip_karg a,
     }
     for (; j < k; ++j) fold4<P>(acc, load4nt(ka->ptrs[j], off, len), ka->tbl + j * P * kTbl);
 #pragma unroll
-    for (int l = 0; l < P; ++l) store4nt(ka->ptrs[k + l], off, acc[l], len);
+    for (int l = 0; l < P; ++l) store4wt(ka->ptrs[k + l], off, acc[l], len);
   } else if (off < len) {
     dot_bytes<P>(ka->ptrs, 0, k, ka->tbl, k, off, static_cast<int>(len - off));
   }
+  karg_done(d, (len & 3) != 0 && blockIdx.x == gridDim.x - 1);
 }
 
 template <int P>
@@ -288,9 +547,11 @@ __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restri
 // One update call whose pointers (source, then P parity rows) and the source's
 // P coefficient tables travel as kernel arguments (as ec_encode_karg).
 template <int P>
-__global__ __launch_bounds__(kBlock) void ec_update_karg(const isal_hip_karg a, int len, unsigned tiles) {
+__global__ __launch_bounds__(kBlock) void ec_update_karg(const isal_hip_karg a, const isal_hip_kdone d, int len,
+                                                         unsigned tiles) {
   const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
-  update_items<P>(ka->ptrs, 1 + P, 0, 1, ka->tbl, len, tiles, tiles, 0);
+  update_items<P, kBufSC1NT>(ka->ptrs, 1 + P, 0, 1, ka->tbl, len, tiles, tiles, 0);
+  karg_done(d, (len & (kVec - 1)) != 0 && blockIdx.x == gridDim.x - 1);
 }
 
 template <int P>
@@ -312,14 +573,46 @@ __global__ __launch_bounds__(kBlock) void ec_update_b1(const uint64_t* __restric
 // ---------------------------------------------------------------------------
 constexpr unsigned kMaxItems = 1u << 30;  // keep w / tiles in 32-bit scalar math
 
-unsigned grid_cap() {
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_GRID_CAP);
-  return v > 0 ? static_cast<unsigned>(v) : 0u;
+// One workgroup per item. (A capped grid striding over the items lost 13-20 %
+// on C2 at 2048-16384 workgroups, profiles/r04_ldsmin_ab.jsonl; the knob that
+// chose it was removed in round 5.)
+unsigned grid_for(unsigned nitems) { return nitems; }
+
+// Ring slots of the LDS-DMA staged wide encode (ec_encode_glds): 0 = off.
+int enc_glds(int P) {
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_GLDS);
+  if (P < 5) return 0;
+  return v == 4 || v == 6 || v == 8 ? static_cast<int>(v) : 0;
 }
 
-unsigned grid_for(unsigned nitems) {
-  const unsigned cap = grid_cap();
-  return (cap && nitems > cap) ? cap : nitems;
+template <int P, int R, int FL>
+void launch_glds(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
+                 const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long r0m,
+                 unsigned c0m) {
+  if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2)
+    fprintf(stderr, "isal_hip: kernel ec_encode_glds<%d, %d, %d>\n", P, R, FL);
+  const size_t lds = ((static_cast<size_t>(k) * P * 8 + 1023) & ~static_cast<size_t>(1023)) + 4u * R * 1024u;
+  hipLaunchKernelGGL((ec_encode_glds<P, R, FL>), dim3(grid), dim3(kBlock), lds, s, ptrs, ptr_stride, src0, dst0, tbl,
+                     len, k, nitems, tiles, r0m, c0m);
+}
+
+template <int P>
+void launch_glds_r(int R, bool x, unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
+                   int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles,
+                   unsigned long long r0m, unsigned c0m) {
+  if constexpr (P >= 5) {
+#define EC_GLDS(r)                                                                                             \
+  if (R == r) {                                                                                                \
+    if (x)                                                                                                     \
+      launch_glds<P, r, kEncXor | kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, \
+                                           c0m);                                                               \
+    else                                                                                                       \
+      launch_glds<P, r, kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);   \
+    return;                                                                                                    \
+  }
+    EC_GLDS(4) EC_GLDS(6) EC_GLDS(8)
+#undef EC_GLDS
+  }
 }
 
 // Passes of 6-8 rows over k = 10, 15, 20, ... sources load in groups of 5
@@ -454,7 +747,9 @@ hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
   const unsigned nitems = nstripes * tiles;
   const unsigned grid = grid_for(nitems);
-  if (vec16) {
+  if (vec16 && enc_glds(P) && enc_order() == 2) {
+    launch_glds_r<P>(enc_glds(P), x, grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+  } else if (vec16) {
     switch (enc_group(k, P)) {
 #define EC_GROUP(u)                                                                                   \
   case u:                                                                                             \
@@ -553,8 +848,11 @@ static bool karg_narrow(int len) {
   return len <= (1 << 20);
 }
 
-extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int k, int rows,
-                                           const isal_hip_encmask* em, void* stream) {
+static const isal_hip_kdone kNoDone = {nullptr, nullptr, nullptr, 0ull};
+
+extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, const isal_hip_kdone* d, int len, int k,
+                                           int rows, const isal_hip_encmask* em, void* stream) {
+  if (!d) d = &kNoDone;
   if (len <= 0 || rows <= 0) return 0;
   if (rows > EC_MAX_ROWS_PER_PASS || k + rows > ISAL_HIP_KARG_PTRS ||
       static_cast<size_t>(kTbl) * k * rows > ISAL_HIP_KARG_TBL)
@@ -565,7 +863,7 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int 
     switch (rows) {
 #define EC_KARG4(n)                                                                                           \
   case n:                                                                                                     \
-    hipLaunchKernelGGL((ec_encode_karg4<n>), dim3(blocks), dim3(kBlock), 0, s, *a, len, k);                  \
+    hipLaunchKernelGGL((ec_encode_karg4<n>), dim3(blocks), dim3(kBlock), 0, s, *a, *d, len, k);              \
     break;
       EC_KARG4(1) EC_KARG4(2) EC_KARG4(3) EC_KARG4(4) EC_KARG4(5) EC_KARG4(6) EC_KARG4(7) EC_KARG4(8)
 #undef EC_KARG4
@@ -583,11 +881,11 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int 
 #define EC_KARG(n, u)                                                                                   \
   case n * 16 + u:                                                                                      \
     if (x)                                                                                              \
-      hipLaunchKernelGGL((ec_encode_karg<n, EncPol<u, kBufNT, kBufNT, 2>, kEncXor>), dim3(tiles),         \
-                         dim3(kBlock), 0, s, *a, len, k, tiles, r0m, c0m);                              \
+      hipLaunchKernelGGL((ec_encode_karg<n, EncPol<u, kBufNT, kBufSC1NT, 2>, kEncXor>), dim3(tiles),      \
+                         dim3(kBlock), 0, s, *a, *d, len, k, tiles, r0m, c0m);                          \
     else                                                                                                \
-      hipLaunchKernelGGL((ec_encode_karg<n, EncPol<u, kBufNT, kBufNT, 2>, kEncLUT>), dim3(tiles),         \
-                         dim3(kBlock), 0, s, *a, len, k, tiles, 0ull, 0u);                              \
+      hipLaunchKernelGGL((ec_encode_karg<n, EncPol<u, kBufNT, kBufSC1NT, 2>, kEncLUT>), dim3(tiles),      \
+                         dim3(kBlock), 0, s, *a, *d, len, k, tiles, 0ull, 0u);                          \
     break;
 #define EC_KARG_U(n) EC_KARG(n, 12) EC_KARG(n, 10) EC_KARG(n, 8) EC_KARG(n, 6) EC_KARG(n, 5) EC_KARG(n, 4)
     EC_KARG_U(1) EC_KARG_U(2) EC_KARG_U(3) EC_KARG_U(4) EC_KARG_U(5) EC_KARG_U(6) EC_KARG_U(7) EC_KARG_U(8)
@@ -599,15 +897,17 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, int len, int 
   return static_cast<int>(hipGetLastError());
 }
 
-extern "C" int isal_hip_launch_update_karg(const isal_hip_karg* a, int len, int rows, void* stream) {
+extern "C" int isal_hip_launch_update_karg(const isal_hip_karg* a, const isal_hip_kdone* d, int len, int rows,
+                                           void* stream) {
   if (len <= 0 || rows <= 0) return 0;
+  if (!d) d = &kNoDone;
   if (rows > EC_MAX_ROWS_PER_PASS) return static_cast<int>(hipErrorInvalidValue);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + kTile - 1) / kTile);
   switch (rows) {
 #define EC_UKARG(n)                                                                                   \
   case n:                                                                                             \
-    hipLaunchKernelGGL(ec_update_karg<n>, dim3(tiles), dim3(kBlock), 0, s, *a, len, tiles);           \
+    hipLaunchKernelGGL(ec_update_karg<n>, dim3(tiles), dim3(kBlock), 0, s, *a, *d, len, tiles);       \
     break;
     EC_UKARG(1) EC_UKARG(2) EC_UKARG(3) EC_UKARG(4) EC_UKARG(5) EC_UKARG(6) EC_UKARG(7) EC_UKARG(8)
 #undef EC_UKARG
@@ -616,33 +916,80 @@ extern "C" int isal_hip_launch_update_karg(const isal_hip_karg* a, int len, int 
   return static_cast<int>(hipGetLastError());
 }
 
+// Load group of the verify kernels: the largest of {10, 8, 6, 4} dividing k,
+// else 4 with the remainder path (fewer instantiations than the encode's
+// enc_group; xor_check / pq_check's usual source counts are covered).
+static int verify_group(int k) {
+  static const int cand[] = {10, 8, 6, 4};
+  for (int u : cand)
+    if (k >= u && k % u == 0) return u;
+  return 4;
+}
+
+template <int P, int U, int FL>
+void launch_verify_v16(unsigned grid, hipStream_t s, const uint64_t* d_ptrs, int ptr_stride, int src_idx0, int dst0,
+                       const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long* out,
+                       int r0, long long col0, unsigned long long r0m, unsigned c0m, unsigned long long* sbad) {
+  hipLaunchKernelGGL((ec_verify_v16<P, EncPol<U, kBufNT, kBufNT, 0>, FL>), dim3(grid), dim3(kBlock), 0, s, d_ptrs,
+                     ptr_stride, src_idx0, dst0, tbl, len, k, nitems, tiles, out, r0, col0, r0m, c0m, sbad);
+}
+
+// One pass of the 16-byte verify (P rows from r0) over nstripes stripes.
+static void verify_pass_v16(int P, int U, bool x, unsigned grid, hipStream_t s, const uint64_t* d_ptrs,
+                            int ptr_stride, int src_idx0, int dst0, const uint32_t* tbl, int len, int k,
+                            unsigned nitems, unsigned tiles, unsigned long long* out, int r0, long long col0,
+                            unsigned long long r0m, unsigned c0m, unsigned long long* sbad) {
+  switch (P * 64 + U * 2 + (x ? 1 : 0)) {
+#define EC_VCASE(n, u)                                                                                          \
+  case n * 64 + u * 2:                                                                                          \
+    launch_verify_v16<n, u, kEncLUT>(grid, s, d_ptrs, ptr_stride, src_idx0, dst0, tbl, len, k, nitems, tiles, out, \
+                                     r0, col0, 0ull, 0u, sbad);                                                 \
+    break;                                                                                                      \
+  case n * 64 + u * 2 + 1:                                                                                      \
+    launch_verify_v16<n, u, kEncXor>(grid, s, d_ptrs, ptr_stride, src_idx0, dst0, tbl, len, k, nitems, tiles, out, \
+                                     r0, col0, r0m, c0m, sbad);                                                 \
+    break;
+#define EC_VCASE_U(n) EC_VCASE(n, 10) EC_VCASE(n, 8) EC_VCASE(n, 6) EC_VCASE(n, 4)
+    EC_VCASE_U(1) EC_VCASE_U(2) EC_VCASE_U(3) EC_VCASE_U(4) EC_VCASE_U(5) EC_VCASE_U(6) EC_VCASE_U(7) EC_VCASE_U(8)
+#undef EC_VCASE_U
+#undef EC_VCASE
+  }
+}
+
 extern "C" int isal_hip_launch_verify(const uint64_t* d_ptrs, int ptr_stride, int src_idx0,
                                       int dst_idx0, const uint32_t* d_tbl, int len, int k, int rows,
                                       long long col0, unsigned long long* slots, int* nslots,
-                                      int vec16, void* stream) {
+                                      int vec16, const isal_hip_encmask* em, void* stream) {
   *nslots = 0;
   if (len <= 0 || rows <= 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  em = enc_xor_masks(em);
   const unsigned span = vec16 ? kTile : kBlock;
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
   const unsigned grid = tiles < EC_VERIFY_MAX_GRID ? tiles : EC_VERIFY_MAX_GRID;
+  const int U = verify_group(k);
   for (int r0 = 0; r0 < rows; r0 += EC_MAX_ROWS_PER_PASS) {
     const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
     const uint32_t* tbl = d_tbl + static_cast<size_t>(kTbl) * k * r0;
     const int dst0 = dst_idx0 + r0;
+    const int g = r0 / EC_MAX_ROWS_PER_PASS;
+    const bool x = em && g < EC_MAX_PASSES && ((em->ok >> g) & 1u);
+    const unsigned long long r0m = x ? em->r0[g] : 0ull;
+    const unsigned c0m = x ? em->c0[g] : 0u;
     unsigned long long* out = slots + *nslots;
-    switch (P) {
-#define EC_CASE(n)                                                                            \
-  case n:                                                                                     \
-    if (vec16)                                                                                \
-      hipLaunchKernelGGL(ec_verify_v16<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride, \
-                         src_idx0, dst0, tbl, len, k, tiles, tiles, out, r0, col0);           \
-    else                                                                                      \
-      hipLaunchKernelGGL(ec_verify_b1<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride,  \
-                         src_idx0, dst0, tbl, len, k, tiles, tiles, out, r0, col0);           \
+    if (!vec16) {
+      switch (P) {
+#define EC_CASE(n)                                                                                      \
+  case n:                                                                                               \
+    hipLaunchKernelGGL(ec_verify_b1<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride, src_idx0, dst0, \
+                       tbl, len, k, tiles, tiles, out, r0, col0);                                       \
     break;
-      EC_CASE(1) EC_CASE(2) EC_CASE(3) EC_CASE(4) EC_CASE(5) EC_CASE(6) EC_CASE(7) EC_CASE(8)
+        EC_CASE(1) EC_CASE(2) EC_CASE(3) EC_CASE(4) EC_CASE(5) EC_CASE(6) EC_CASE(7) EC_CASE(8)
 #undef EC_CASE
+      }
+    } else {
+      verify_pass_v16(P, U, x, grid, s, d_ptrs, ptr_stride, src_idx0, dst0, tbl, len, k, tiles, tiles, out, r0, col0,
+                      r0m, c0m, nullptr);
     }
     *nslots += static_cast<int>(grid);
     isal_hip_count_launch();
@@ -650,6 +997,67 @@ extern "C" int isal_hip_launch_verify(const uint64_t* d_ptrs, int ptr_stride, in
     if (e != hipSuccess) return static_cast<int>(e);
   }
   return 0;
+}
+
+extern "C" int isal_hip_launch_verify_batch(const uint64_t* d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
+                                            const uint32_t* d_tbl, int len, int k, int rows, long long nstripes,
+                                            const isal_hip_encmask* em, unsigned long long* bad, void* stream) {
+  if (len <= 0 || rows <= 0 || nstripes <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(bad, 0xff, static_cast<size_t>(nstripes) * 8, s);
+  if (e != hipSuccess) return static_cast<int>(e);
+  em = enc_xor_masks(em);
+  const unsigned per = stripes_per_launch(len, true);
+  const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + kTile - 1) / kTile);
+  const int U = verify_group(k);
+  for (long long s0 = 0; s0 < nstripes; s0 += per) {
+    const unsigned ns = static_cast<unsigned>(nstripes - s0 < per ? nstripes - s0 : per);
+    const uint64_t* ptrs = d_ptrs + s0 * ptr_stride;
+    for (int r0 = 0; r0 < rows; r0 += EC_MAX_ROWS_PER_PASS) {
+      const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
+      const int g = r0 / EC_MAX_ROWS_PER_PASS;
+      const bool x = em && g < EC_MAX_PASSES && ((em->ok >> g) & 1u);
+      verify_pass_v16(P, U, x, ns * tiles, s, ptrs, ptr_stride, src_idx0, dst_idx0 + r0,
+                      d_tbl + static_cast<size_t>(kTbl) * k * r0, len, k, ns * tiles, tiles, nullptr, r0, 0,
+                      x ? em->r0[g] : 0ull, x ? em->c0[g] : 0u, bad + s0);
+      isal_hip_count_launch();
+      e = hipGetLastError();
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+  }
+  return 0;
+}
+
+extern "C" int isal_hip_launch_verify_karg(const isal_hip_karg* a, const isal_hip_kdone* d, int len, int k,
+                                           int rows, const isal_hip_encmask* em, void* stream) {
+  if (len <= 0 || rows <= 0) return 0;
+  if (!d || !d->cnt || !d->res || !d->mail || rows > EC_MAX_ROWS_PER_PASS || k + rows > ISAL_HIP_KARG_PTRS ||
+      static_cast<size_t>(kTbl) * k * rows > ISAL_HIP_KARG_TBL)
+    return static_cast<int>(hipErrorInvalidValue);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + kTile - 1) / kTile);
+  em = enc_xor_masks(em);
+  const bool x = em && (em->ok & 1u);
+  const unsigned long long r0m = x ? em->r0[0] : 0ull;
+  const unsigned c0m = x ? em->c0[0] : 0u;
+  switch (rows * 64 + verify_group(k) * 2 + (x ? 1 : 0)) {
+#define EC_VKARG(n, u)                                                                                             \
+  case n * 64 + u * 2:                                                                                             \
+    hipLaunchKernelGGL((ec_verify_karg<n, EncPol<u, kBufNT, kBufNT, 0>, kEncLUT>), dim3(tiles), dim3(kBlock), 0, s, \
+                       *a, *d, len, k, tiles, 0ull, 0u);                                                           \
+    break;                                                                                                         \
+  case n * 64 + u * 2 + 1:                                                                                         \
+    hipLaunchKernelGGL((ec_verify_karg<n, EncPol<u, kBufNT, kBufNT, 0>, kEncXor>), dim3(tiles), dim3(kBlock), 0, s, \
+                       *a, *d, len, k, tiles, r0m, c0m);                                                           \
+    break;
+#define EC_VKARG_U(n) EC_VKARG(n, 10) EC_VKARG(n, 8) EC_VKARG(n, 6) EC_VKARG(n, 4)
+    EC_VKARG_U(1) EC_VKARG_U(2) EC_VKARG_U(3) EC_VKARG_U(4) EC_VKARG_U(5) EC_VKARG_U(6) EC_VKARG_U(7) EC_VKARG_U(8)
+#undef EC_VKARG_U
+#undef EC_VKARG
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
+  isal_hip_count_launch();
+  return static_cast<int>(hipGetLastError());
 }
 
 extern "C" int isal_hip_launch_update(const uint64_t* d_ptrs, int ptr_stride, int src_idx,

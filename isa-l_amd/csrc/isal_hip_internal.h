@@ -47,7 +47,8 @@ size_t isal_hip_tables_dwords(int k, int rows);
  * `ok` — when its first row and its column of source 0 hold only 0 and 1 and
  * k <= 64; then r0[g] has bit j set where row 8g's coefficient of source j is
  * 1, and c0[g] bit l where row 8g + l's coefficient of source 0 is 1.
- * ISAL_HIP_ENC_XOR=0 clears `ok` (every pass takes the lookup path). */
+ * The masks are computed whatever the knobs say; ISAL_HIP_ENC_XOR=0 makes the
+ * launch ignore them (every pass takes the lookup path). */
 #define EC_MAX_PASSES 32
 typedef struct {
         unsigned ok;
@@ -72,11 +73,39 @@ typedef struct {
         uint64_t ptrs[ISAL_HIP_KARG_PTRS];
         uint32_t tbl[ISAL_HIP_KARG_TBL];
 } isal_hip_karg;
-int isal_hip_launch_encode_karg(const isal_hip_karg *a, int len, int k, int rows,
+/* Completion of a kernel-argument call without the runtime's wake-up: every
+ * workgroup publishes its stores (agent-scope release) and counts itself in
+ * *cnt; the last one resets *cnt (and *res) for the next call and writes
+ * mail[1] = the verify result (*res, ~0 for encode / update), then mail[0] =
+ * seq (system-scope release) into page-locked host memory that the calling
+ * thread spins on (isal_hip_shim.c wait_done). cnt = NULL: no protocol (the
+ * caller synchronises the stream). res: device word a verify's mismatching
+ * lanes atomically lower (~0 between calls); NULL for encode / update. */
+typedef struct {
+        unsigned *cnt;
+        unsigned long long *res;
+        unsigned long long *mail; /* device view of the host mailbox */
+        unsigned long long seq;
+} isal_hip_kdone;
+/* cnt: ISAL_HIP_KDONE_GROUPS group counters ISAL_HIP_KDONE_STRIDE words apart
+ * (one 64-byte line each), then the top counter: workgroups count in groups
+ * of max(32, ceil(n / GROUPS)) and each group's last one counts in the top
+ * counter — at most 256 atomics on any one word instead of one per workgroup
+ * (a single word serialised 1024 workgroups' atomics: +10 us per call). */
+#define ISAL_HIP_KDONE_GROUPS 256
+#define ISAL_HIP_KDONE_STRIDE 16
+#define ISAL_HIP_KDONE_WORDS ((ISAL_HIP_KDONE_GROUPS + 1) * ISAL_HIP_KDONE_STRIDE)
+int isal_hip_launch_encode_karg(const isal_hip_karg *a, const isal_hip_kdone *d, int len, int k, int rows,
                                 const isal_hip_encmask *em, void *stream);
 /* ec_encode_data_update of one stripe the same way: ptrs = {source, rows
  * parity}, tbl = the source's tables for rows <= EC_MAX_ROWS_PER_PASS outputs. */
-int isal_hip_launch_update_karg(const isal_hip_karg *a, int len, int rows, void *stream);
+int isal_hip_launch_update_karg(const isal_hip_karg *a, const isal_hip_kdone *d, int len, int rows,
+                                void *stream);
+/* Verify of one stripe the same way (ptrs = k sources then rows stored
+ * outputs, tables as for the encode): the first mismatch, key (column << 8 |
+ * row), arrives in mail[1] (~0: none). Needs d->cnt, d->res and d->mail. */
+int isal_hip_launch_verify_karg(const isal_hip_karg *a, const isal_hip_kdone *d, int len, int k, int rows,
+                                const isal_hip_encmask *em, void *stream);
 int isal_hip_launch_update(const uint64_t *d_ptrs, int ptr_stride, int src_idx, int dst_idx0,
                            const uint32_t *d_tbl, int len, int k, int rows, int vec_i,
                            long long nstripes, int vec16, void *stream);
@@ -91,7 +120,16 @@ int isal_hip_launch_update(const uint64_t *d_ptrs, int ptr_stride, int src_idx, 
         ((((rows) + EC_MAX_ROWS_PER_PASS - 1) / EC_MAX_ROWS_PER_PASS) * EC_VERIFY_MAX_GRID)
 int isal_hip_launch_verify(const uint64_t *d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
                            const uint32_t *d_tbl, int len, int k, int rows, long long col0,
-                           unsigned long long *slots, int *nslots, int vec16, void *stream);
+                           unsigned long long *slots, int *nslots, int vec16, const isal_hip_encmask *em,
+                           void *stream);
+
+/* Verify every stripe of a batch (16-byte aligned shards): bad[s] = ~0 when
+ * stripe s's stored rows equal its recomputed parity, else its first
+ * mismatch as column << 8 | row (bad: device memory, nstripes words, set on
+ * the stream before the kernels). */
+int isal_hip_launch_verify_batch(const uint64_t *d_ptrs, int ptr_stride, int src_idx0, int dst_idx0,
+                                 const uint32_t *d_tbl, int len, int k, int rows, long long nstripes,
+                                 const isal_hip_encmask *em, unsigned long long *bad, void *stream);
 
 /* The shim's generic synchronous call (host or device shard pointers).
  * op: ISAL_HIP_OP_ENCODE (dst = coded sources, nsrc = k), ISAL_HIP_OP_UPDATE
@@ -128,7 +166,7 @@ enum {
         ISAL_HIP_KNOB_LOG,           /* 1: log every drop-in call's route to stderr */
         ISAL_HIP_KNOB_CPU_SIMD,      /* CPU route width cap: 0 per byte, 1 AVX2, 2 GFNI (tests) */
         ISAL_HIP_KNOB_STAGE_MB,
-        ISAL_HIP_KNOB_GRID_CAP,
+        ISAL_HIP_KNOB_ENC_GLDS,      /* wide encode passes staged through LDS by LDS-DMA: ring slots 4|6|8, 0 off */
         ISAL_HIP_KNOB_CRC_TILES,
         ISAL_HIP_KNOB_CRC_STEP,
         ISAL_HIP_KNOB_CRC_SRC_CHAIN, /* lds(0) | reg(1) */
@@ -158,7 +196,7 @@ enum {
         ISAL_HIP_KNOB_ENC_LDS,         /* encode low table halves from LDS: 1 always, 0 never (default: 5-6 looked-up rows) */
         ISAL_HIP_KNOB_KARG,            /* 0: device-resident drop-in encodes upload their arguments */
         ISAL_HIP_KNOB_MAX_HELPERS,     /* copy-out helper threads per process (default 8) */
-        ISAL_HIP_KNOB_SYNC_SPIN,       /* 1: synchronous calls poll hipStreamQuery instead of blocking (A/B) */
+        ISAL_HIP_KNOB_KARG_DONE,       /* 0: kernel-argument calls wait in hipStreamSynchronize (no host mailbox) */
         ISAL_HIP_KNOB_ENC_GROUP,       /* 12/10/8/6/5/4: encode load group forced (tuning A/B) */
         ISAL_HIP_KNOB_KARG_NARROW,     /* drop-in kernel-argument encode with 4-byte lanes: 1 on, 0 off */
         ISAL_HIP_KNOB_ENC_WIDE5,       /* 0: 6-8 row passes keep the largest load group (no groups of 5) */

@@ -29,7 +29,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_LOG] = {"ISAL_HIP_LOG", NULL},
         [ISAL_HIP_KNOB_CPU_SIMD] = {"ISAL_HIP_CPU_SIMD", NULL},
         [ISAL_HIP_KNOB_STAGE_MB] = {"ISAL_HIP_STAGE_MB", NULL},
-        [ISAL_HIP_KNOB_GRID_CAP] = {"ISAL_HIP_GRID_CAP", NULL},
+        [ISAL_HIP_KNOB_ENC_GLDS] = {"ISAL_HIP_ENC_GLDS", NULL},
         [ISAL_HIP_KNOB_CRC_TILES] = {"ISAL_HIP_CRC_TILES", NULL},
         [ISAL_HIP_KNOB_CRC_STEP] = {"ISAL_HIP_CRC_STEP", NULL},
         [ISAL_HIP_KNOB_CRC_SRC_CHAIN] = {"ISAL_HIP_CRC_SRC_CHAIN", chain_words},
@@ -59,7 +59,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_ENC_LDS] = {"ISAL_HIP_ENC_LDS", NULL},
         [ISAL_HIP_KNOB_KARG] = {"ISAL_HIP_KARG", NULL},
         [ISAL_HIP_KNOB_MAX_HELPERS] = {"ISAL_HIP_MAX_HELPERS", NULL},
-        [ISAL_HIP_KNOB_SYNC_SPIN] = {"ISAL_HIP_SYNC_SPIN", NULL},
+        [ISAL_HIP_KNOB_KARG_DONE] = {"ISAL_HIP_KARG_DONE", NULL},
         [ISAL_HIP_KNOB_ENC_GROUP] = {"ISAL_HIP_ENC_GROUP", NULL},
         [ISAL_HIP_KNOB_KARG_NARROW] = {"ISAL_HIP_KARG_NARROW", NULL},
         [ISAL_HIP_KNOB_ENC_WIDE5] = {"ISAL_HIP_ENC_WIDE5", NULL},

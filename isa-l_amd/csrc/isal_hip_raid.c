@@ -18,9 +18,9 @@
 #include "isal_hip_internal.h"
 
 /* gftbls (base format: byte 1 of each 32-B entry is the coefficient) for
- * rows = 1 (P) or 2 (P, Q) over n sources. Caller frees. */
+ * rows = 1 (P) or 2 (P, Q) over n sources. */
 static unsigned char *
-raid_tables(int n, int rows)
+raid_build(int n, int rows)
 {
         unsigned char *t = (unsigned char *) calloc((size_t) 32 * n * rows, 1);
         unsigned char q = 1;
@@ -37,16 +37,49 @@ raid_tables(int n, int rows)
         return t;
 }
 
+/* The tables for up to RAID_CACHE_MAX sources are built once per (n, rows)
+ * and shared by every later call and thread (immutable once published), so
+ * a RAID call allocates nothing and the shim's per-thread table cache finds
+ * the same coefficients call after call. *owned: the caller frees it. */
+#define RAID_CACHE_MAX 255
+static unsigned char *raid_cache[2][RAID_CACHE_MAX + 1];
+
+static const unsigned char *
+raid_tables(int n, int rows, int *owned)
+{
+        unsigned char *t, *want = NULL;
+        *owned = 0;
+        if (n < 1 || rows < 1 || rows > 2)
+                return NULL;
+        if (n > RAID_CACHE_MAX) {
+                *owned = 1;
+                return raid_build(n, rows);
+        }
+        t = __atomic_load_n(&raid_cache[rows - 1][n], __ATOMIC_ACQUIRE);
+        if (t)
+                return t;
+        if (!(t = raid_build(n, rows)))
+                return NULL;
+        if (!__atomic_compare_exchange_n(&raid_cache[rows - 1][n], &want, t, 0, __ATOMIC_ACQ_REL,
+                                         __ATOMIC_ACQUIRE)) {
+                free(t); /* another thread published the same table first */
+                return want;
+        }
+        return t;
+}
+
 static int
 raid_run(int op, int len, int nsrc, int rows, void **array)
 {
-        unsigned char *t = raid_tables(nsrc, rows);
+        int owned;
+        const unsigned char *t = raid_tables(nsrc, rows, &owned);
         unsigned long long bad;
         if (!t)
                 return 1;
         bad = isal_hip_run(op, len, nsrc, rows, 0, t, (unsigned char *const *) array, nsrc,
                            (unsigned char *const *) array + nsrc);
-        free(t);
+        if (owned)
+                free((void *) t);
         if (op != ISAL_HIP_OP_VERIFY || bad == ~0ull)
                 return 0;
         /* reference pq_check_base: i | 1 when P differs at byte i, else i | 2 */

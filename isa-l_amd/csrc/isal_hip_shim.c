@@ -31,10 +31,12 @@
  */
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "erasure_code.h"
 #include "isal_hip.h"
@@ -215,6 +217,15 @@ typedef struct {
         uint32_t *ttbl;
         size_t tcap_coef, tcap_tbl;
         isal_hip_encmask tem;
+        /* completion of kernel-argument calls (isal_hip_kdone): device words
+         * {arrival counter, verify result}, the page-locked host mailbox
+         * {seq, result} and its device view, the last sequence number, and
+         * calls since the stream was last synchronised */
+        void *d_done;
+        volatile unsigned long long *h_mail;
+        void *h_mail_dev;
+        unsigned long long seq;
+        int unsynced;
 } ctx_t;
 
 /* Copy-out worker of a calling thread. The runtime serves a copy from or to
@@ -283,6 +294,10 @@ ctx_release(void *p)
                 (void) hipHostFree(c->h_args);
         if (c->d_stage)
                 (void) hipFree(c->d_stage);
+        if (c->d_done)
+                (void) hipFree(c->d_done);
+        if (c->h_mail)
+                (void) hipHostFree((void *) c->h_mail);
         if (c->oq)
                 outq_stop(c);
         free(c->jobs);
@@ -642,7 +657,7 @@ launch_op(ctx_t *c, int op, char *args, const layout_t *L, int nptr, int nsrc, i
         if (op == OP_VERIFY)
                 return (hipError_t) isal_hip_launch_verify(
                         ptrs, nptr, 0, nsrc, tbl, clen, k, rows, c0,
-                        (unsigned long long *) (args + L->slots_off), nslots, vec16, c->stream);
+                        (unsigned long long *) (args + L->slots_off), nslots, vec16, em, c->stream);
         if (op == OP_ENCODE)
                 return (hipError_t) isal_hip_launch_encode(ptrs, nptr, 0, nsrc, tbl, clen, k, rows,
                                                            1, vec16, em, c->stream);
@@ -1391,41 +1406,129 @@ karg_fits(int op, int len, int k, int rows, const uint64_t *view, int nptr)
         return 1;
 }
 
-/* The end of a kernel-argument call: hipStreamSynchronize, or with
- * ISAL_HIP_SYNC_SPIN=1 a poll of hipStreamQuery (an A/B of the wake-up
- * latency; the call trace shows ~9 us between the kernel's end and the
- * synchronisation returning, profiles/r04_dropin_hiptrace_b.txt). */
+/* The completion words of kernel-argument calls, allocated on a thread's
+ * first such call: device {counters = 0 (isal_hip_kdone), verify result = ~0}, host mailbox
+ * (page-locked, coherent: the kernel's system-scope stores land in it with no
+ * cached copy in between). */
+#define KDONE_CNT_BYTES ((size_t) ISAL_HIP_KDONE_WORDS * 4)
 static hipError_t
-sync_call(hipStream_t s)
+ensure_done(ctx_t *c)
 {
+        static const unsigned long long res_init = ~0ull;
         hipError_t e;
-        if (isal_hip_knob(ISAL_HIP_KNOB_SYNC_SPIN) != 1)
-                return hipStreamSynchronize(s);
-        while ((e = hipStreamQuery(s)) == hipErrorNotReady)
-                __builtin_ia32_pause();
-        return e;
+        void *h = NULL;
+        if (c->d_done)
+                return hipSuccess;
+        if ((e = hipMalloc(&c->d_done, KDONE_CNT_BYTES + 64)) != hipSuccess)
+                return e;
+        if ((e = hipMemset(c->d_done, 0, KDONE_CNT_BYTES)) != hipSuccess ||
+            (e = hipMemcpy((char *) c->d_done + KDONE_CNT_BYTES, &res_init, 8, hipMemcpyHostToDevice)) !=
+                    hipSuccess ||
+            (e = hipHostMalloc(&h, 64, hipHostMallocCoherent)) != hipSuccess ||
+            (e = hipHostGetDevicePointer(&c->h_mail_dev, h, 0)) != hipSuccess) {
+                (void) hipFree(c->d_done);
+                if (h)
+                        (void) hipHostFree(h);
+                c->d_done = NULL;
+                return e;
+        }
+        memset(h, 0, 64);
+        c->h_mail = (volatile unsigned long long *) h;
+        return hipSuccess;
 }
 
+static double
+now_s(void)
+{
+        struct timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        return (double) t.tv_sec + 1e-9 * (double) t.tv_nsec;
+}
+
+/* Wait for call `seq` of this thread: spin on the mailbox the kernel's last
+ * workgroup writes (the runtime's completion signal and wake-up cost ~9 us
+ * more). Bounded: after SPIN_S seconds without it the stream is
+ * synchronised, so a kernel that faulted is reported through the runtime and
+ * a slow one is simply waited for. The stream is still synchronised every
+ * SYNC_EVERY calls (the kernels have long ended by then) so the runtime
+ * retires its launch records. */
+#define DONE_SPIN_S 0.02
+#define DONE_YIELD_S 50e-6 /* then yield the CPU between polls: callers may outnumber cores */
+#define DONE_SYNC_EVERY 64
+static hipError_t
+wait_done(ctx_t *c, unsigned long long seq)
+{
+        hipError_t e;
+        unsigned spins = 0;
+        int yield = 0;
+        double t0 = 0;
+        while (c->h_mail[0] != seq) {
+                if (yield)
+                        sched_yield();
+                else
+                        __builtin_ia32_pause();
+                if ((++spins & 63) == 0) {
+                        const double t = now_s();
+                        if (t0 == 0)
+                                t0 = t;
+                        else if (t - t0 > DONE_SPIN_S)
+                                break;
+                        else
+                                yield = t - t0 > DONE_YIELD_S;
+                }
+        }
+        if (c->h_mail[0] != seq) {
+                if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
+                        return e;
+                c->unsynced = 0;
+                if (c->h_mail[0] != seq)
+                        return hipErrorUnknown; /* the kernel ended without writing its completion word */
+                return hipSuccess;
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE); /* the result word was written before seq */
+        if (++c->unsynced >= DONE_SYNC_EVERY) {
+                c->unsynced = 0;
+                return hipStreamSynchronize(c->stream);
+        }
+        return hipSuccess;
+}
+
+/* A kernel-argument call's arguments, in the 2 KiB block the kernels read
+ * from their kernarg segment. mail: the completion mailbox is used (every
+ * shard is hipMalloc memory: managed memory the host may read directly is
+ * left to hipStreamSynchronize, which also makes the host's view coherent;
+ * ISAL_HIP_KARG_DONE=0 turns the mailbox off). A verify needs the mailbox. */
 static gpu_res
 gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *view, const uint32_t *tbl,
-         const isal_hip_encmask *em)
+         const isal_hip_encmask *em, int mail)
 {
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         const int nsrc = op == OP_UPDATE ? 1 : k;
+        isal_hip_kdone d = {NULL, NULL, NULL, 0ull};
         isal_hip_karg a;
+        hipError_t e;
         memset(&a, 0, sizeof(a));
         memcpy(a.ptrs, view, sizeof(uint64_t) * (size_t) (nsrc + rows));
+        if (mail) {
+                GPU_TRY_AT(r, FAULT_ALLOC, ensure_done(c));
+                d.cnt = (unsigned *) c->d_done;
+                d.res = op == OP_VERIFY ? (unsigned long long *) ((char *) c->d_done + KDONE_CNT_BYTES) : NULL;
+                d.mail = (unsigned long long *) c->h_mail_dev;
+                d.seq = ++c->seq;
+        }
         if (op == OP_UPDATE) {
                 /* one pass: source vec_i's tables for every row are contiguous */
                 memcpy(a.tbl, tbl + isal_hip_tables_dwords(vec_i, rows), isal_hip_tables_dwords(1, rows) * 4);
-                GPU_TRY_AT(r, FAULT_LAUNCH, (hipError_t) isal_hip_launch_update_karg(&a, len, rows, c->stream));
-                GPU_TRY_AT(r, FAULT_SYNC, sync_call(c->stream));
-                r.done = len;
-                return r;
+                e = (hipError_t) isal_hip_launch_update_karg(&a, &d, len, rows, c->stream);
+        } else {
+                memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
+                e = (hipError_t) (op == OP_VERIFY ? isal_hip_launch_verify_karg(&a, &d, len, k, rows, em, c->stream)
+                                                  : isal_hip_launch_encode_karg(&a, &d, len, k, rows, em, c->stream));
         }
-        memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
-        GPU_TRY_AT(r, FAULT_LAUNCH, (hipError_t) isal_hip_launch_encode_karg(&a, len, k, rows, em, c->stream));
-        GPU_TRY_AT(r, FAULT_SYNC, sync_call(c->stream));
+        GPU_TRY_AT(r, FAULT_LAUNCH, e);
+        GPU_TRY_AT(r, FAULT_SYNC, mail ? wait_done(c, d.seq) : hipStreamSynchronize(c->stream));
+        if (op == OP_VERIFY)
+                r.first_bad = c->h_mail[1];
         r.done = len;
         return r;
 }
@@ -1456,7 +1559,7 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         const isal_hip_encmask *em = &no_masks;
         const uint32_t *tbl = NULL;
         seen_t sn;
-        int i, nstage = 0, ndev = 0, all_host, cur_dev;
+        int i, nstage = 0, ndev = 0, nplain = 0, all_host, cur_dev, mail;
         size_t bytes;
         gpu_res r;
         ctx_t *c;
@@ -1504,6 +1607,7 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                                 seen_add(&sn, rb, rs);
                 }
                 is_dev = kind != CL_HOST;
+                nplain += kind == CL_DEVICE;
                 /* An update's parity in page-locked host memory is staged, not
                  * written in place: a kernel that failed after it started could
                  * have folded some of it already, and the CPU fallback could not
@@ -1530,14 +1634,16 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 r.what = "ctx_tables (host memory)";
                 c = NULL;
         }
-        if (c && op != OP_ENCODE)
+        if (c && op == OP_UPDATE)
                 em = &no_masks;
         if (!c) {
                 r.done = 0;
                 r.first_bad = ~0ull;
-        } else if (ndev == nptr && op != OP_VERIFY && karg_fits(op, len, k, rows, view, nptr)) {
+        } else if (ndev == nptr && (mail = nplain == nptr && isal_hip_knob(ISAL_HIP_KNOB_KARG_DONE) != 0,
+                                    op != OP_VERIFY || mail) &&
+                   karg_fits(op, len, k, rows, view, nptr)) {
                 route_log(op, len, k, rows, "gpu kernel-args", "device shards");
-                r = gpu_karg(c, op, len, k, rows, vec_i, view, tbl, em);
+                r = gpu_karg(c, op, len, k, rows, vec_i, view, tbl, em, mail);
         } else if (bytes <= ZC_BYTES || (nstage && (size_t) len * (size_t) nstage <= PACK_BYTES)) {
                 const int zc = bytes <= ZC_BYTES;
                 route_log(op, len, k, rows, zc ? "gpu zero-copy" : "gpu packed",
@@ -1793,6 +1899,17 @@ isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream)
                 return ISAL_HIP_EINVAL;
         return isal_hip_launch_update(b->d_ptrs, b->k + b->rows, vec_i, b->k, b->d_tbl, b->len,
                                       b->k, b->rows, vec_i, b->nstripes, b->vec16, stream)
+                       ? ISAL_HIP_EHIP
+                       : ISAL_HIP_OK;
+}
+
+int
+isal_hip_batch_check(isal_hip_batch *b, unsigned long long *bad, void *stream)
+{
+        if (!b || !bad || !b->vec16)
+                return ISAL_HIP_EINVAL;
+        return isal_hip_launch_verify_batch(b->d_ptrs, b->k + b->rows, 0, b->k, b->d_tbl, b->len, b->k, b->rows,
+                                            b->nstripes, &b->em, bad, stream)
                        ? ISAL_HIP_EHIP
                        : ISAL_HIP_OK;
 }

@@ -298,6 +298,14 @@ class Batch:
         if rc != 0:
             raise RuntimeError(f"isal_hip_batch_update failed ({rc})")
 
+    def check(self, bad, stream: int = 0) -> None:
+        """Verify every stripe (isal_hip_batch_check): the DEVICE buffer bad
+        (nstripes uint64) gets ~0 for a consistent stripe, else its first
+        mismatch as column << 8 | row."""
+        rc = lib().isal_hip_batch_check(self._h, ctypes.c_void_p(addr(bad)), ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"isal_hip_batch_check failed ({rc})")
+
     def encode_crc(self, init: int, crc, stream: int = 0) -> None:
         """encode() plus crc32_iscsi(shard, len, init) of every source and parity
         shard into the DEVICE buffer crc (nstripes*(k+rows) uint32, stripe-major,

@@ -2020,3 +2020,188 @@ def test_k0_empty_sum_on_a_fresh_thread(engine, gpu, monkeypatch, backend):
     assert "err" not in out, out.get("err")
     assert all(not p.any() for p in out["par"])
     assert engine.kernel_launches() > launches and engine.fallbacks() == fb
+
+
+def test_dropin_result_visible_to_other_streams(engine, oracle, gpu):
+    """A kernel-argument call returns when its kernel's last workgroup has
+    written the host mailbox (isal_hip_kdone), before the runtime has seen the
+    kernel end: the parity must already be visible to work the caller issues
+    right away on a NON-blocking stream (no implicit ordering with the
+    engine's stream) — a copy to the host and a kernel reading it."""
+    import torch
+
+    k, rows, n = 10, 4, 256 << 10
+    coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+    tbls = engine.ec_init_tables(k, rows, coef)
+    src = torch.empty((k, n), dtype=torch.uint8, device=gpu)
+    out = torch.zeros((rows, n), dtype=torch.uint8, device=gpu)
+    side = torch.cuda.Stream(device=gpu)
+    pin = torch.empty((rows, n), dtype=torch.uint8).pin_memory()
+    for it in range(24):
+        src.random_(generator=torch.Generator(device=gpu).manual_seed(100 + it))
+        torch.cuda.synchronize()
+        engine.ec_encode_data(n, k, rows, tbls, [src[j] for j in range(k)], [out[l] for l in range(rows)])
+        with torch.cuda.stream(side):
+            pin.copy_(out, non_blocking=True)
+            x = out[0].clone()  # a kernel on the side stream reading row 0
+        side.synchronize()
+        h = _host(src)
+        want = oracle.encode(coef, k, rows, [h[j] for j in range(k)])
+        for l in range(rows):
+            assert np.array_equal(pin[l].numpy(), want[l]), (it, l)
+        assert np.array_equal(_host(x), want[0]), it
+
+
+@pytest.mark.parametrize("done", ["1", "0"])
+def test_dropin_completion_paths_vs_oracle(engine, oracle, gpu, monkeypatch, done):
+    """Encode, update and verify on device shards through the kernel-argument
+    route with the host mailbox (default) and with ISAL_HIP_KARG_DONE=0
+    (hipStreamSynchronize; a verify then takes the generic route): == oracle,
+    many calls in a row (the counter and result words reset themselves) and
+    from four threads at once (one mailbox per thread)."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_KARG_DONE", done)
+    pc = _raid_fn(engine, "pq_check")
+    errors = []
+
+    def worker(t):
+        try:
+            k, rows, n = 6 + t, 2 + t % 3, 4096 * (3 + t) + 16 * t
+            coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+            tbls = engine.ec_init_tables(k, rows, coef)
+            g = torch.Generator(device=gpu).manual_seed(t)
+            for it in range(20):
+                src = torch.empty((k, n), dtype=torch.uint8, device=gpu)
+                src.random_(generator=g)
+                out = torch.full((rows, n), 0xAB, dtype=torch.uint8, device=gpu)
+                torch.cuda.synchronize()
+                engine.ec_encode_data(n, k, rows, tbls, [src[j] for j in range(k)], [out[l] for l in range(rows)])
+                h = _host(src)
+                want = oracle.encode(coef, k, rows, [h[j] for j in range(k)])
+                if not all(np.array_equal(_host(out[l]), want[l]) for l in range(rows)):
+                    errors.append(("encode", t, it))
+                upd = torch.zeros((rows, n), dtype=torch.uint8, device=gpu)
+                for v in range(k):
+                    engine.ec_encode_data_update(n, k, rows, v, tbls, src[v], [upd[l] for l in range(rows)])
+                if not torch.equal(upd, out):
+                    errors.append(("update", t, it))
+            # verify (pq_check) on device shards, consistent then corrupted
+            v, n2 = 4 + t, 8192 + 32 * t
+            bufs = [torch.from_numpy(fill_bytes(n2, 500 + 10 * t + j)).to(gpu) for j in range(v)]
+            if _raid_fn(engine, "pq_gen")(v, n2, _vp(bufs)) != 0 or pc(v, n2, _vp(bufs)) != 0:
+                errors.append(("pq_check clean", t))
+            for it in range(6):
+                j, i = (t + it) % v, (977 * it + 13 * t) % n2
+                old = int(bufs[j][i])
+                bufs[j][i] = old ^ 0x04
+                want = [b.cpu().numpy() for b in bufs]
+                got = pc(v, n2, _vp(bufs))
+                bufs[j][i] = old
+                want[j][i] = old
+                ref = [w.copy() for w in want]
+                ref[j][i] ^= 0x04
+                if got != oracle.raid("pq_check", v, n2, ref):
+                    errors.append(("pq_check", t, it, got))
+                if pc(v, n2, _vp(bufs)) != 0:
+                    errors.append(("pq_check after", t, it))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errors, errors
+
+
+@pytest.mark.parametrize("xor", ["1", "0"])
+@pytest.mark.parametrize("karg", ["1", "0"])
+@pytest.mark.parametrize("v", [3, 4, 6, 8, 12, 18, 22, 32])
+def test_raid_check_routes_vs_oracle(engine, oracle, gpu, monkeypatch, xor, karg, v):
+    """xor_check / pq_check on device shards: the kernel-argument verify
+    (default; source counts hitting every load group 10/8/6/4 and the
+    remainder path) and the generic verify (ISAL_HIP_KARG=0), with the 0/1
+    XOR path on and off; every result == the oracle's (raid_base.c:96-99
+    encoding), corruption in sources, P and Q, near the tail and the start."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_ENC_XOR", xor)
+    _setenv(monkeypatch, "ISAL_HIP_KARG", karg)
+    xc, pc, pg, xg = (_raid_fn(engine, f) for f in ("xor_check", "pq_check", "pq_gen", "xor_gen"))
+    n = 4096 * 2 + 96
+    h = [fill_bytes(n, 40 * v + j) for j in range(v)]
+    hx = [a.copy() for a in h]
+    assert oracle.raid("pq_gen", v, n, h) == 0 if v >= 4 else True
+    assert oracle.raid("xor_gen", v, n, hx) == 0
+    bp = [torch.from_numpy(a).to(gpu) for a in h]
+    bx = [torch.from_numpy(a).to(gpu) for a in hx]
+    if v >= 4:
+        assert pc(v, n, _vp(bp)) == 0
+    assert xc(v, n, _vp(bx)) == 0
+    for j, i in [(0, 0), (v - 1, n - 1), (v // 2, n // 2), (1, 4095), (v - 2, 17)]:
+        for bufs, host, f, name in ((bp, h, pc, "pq_check"), (bx, hx, xc, "xor_check")):
+            if name == "pq_check" and v < 4:
+                continue
+            old = int(bufs[j][i])
+            bufs[j][i] = old ^ 0x80
+            ref = [a.copy() for a in host]
+            ref[j][i] ^= 0x80
+            got = f(v, n, _vp(bufs))
+            bufs[j][i] = old
+            assert got == oracle.raid(name, v, n, ref), (name, j, i, got)
+
+
+@pytest.mark.parametrize("xor", ["1", "0"])
+@pytest.mark.parametrize("k,rows,n,ns", [
+    (10, 2, 65536, 24),      # RAID-6 shape: XOR path, group 10
+    (8, 1, 4096 * 5, 16),    # RAID-5
+    (10, 4, 4096 * 3 + 48, 9),  # RS rows, ragged tail
+    (7, 3, 8192, 8),         # k % 4 remainder
+    (12, 12, 4096 * 2, 5),   # two passes (rows > 8)
+    (24, 6, 4096 * 4, 8),    # group 8... (24 % 10 != 0)
+])
+def test_batch_check_vs_oracle(engine, oracle, gpu, monkeypatch, xor, k, rows, n, ns):
+    """isal_hip_batch_check: bad[s] = ~0 for consistent stripes, else the first
+    mismatch (smallest column, then row) — computed here from the oracle's
+    parity — for corruption in sources and in any parity row, two passes."""
+    import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_ENC_XOR", xor)
+    if rows <= 2:  # RAID P (+ Q = 2^j): raid_base.c:44-68
+        coef = np.ones(k * rows, np.uint8)
+        q = 1
+        for j in range(k * (rows - 1)):
+            coef[k + j] = q
+            q = engine.gf_mul(q, 2)
+    else:
+        coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:] if k + rows <= 32 else fill_bytes(k * rows, k + rows)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 17 + k)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.encode(0)
+    bad = torch.zeros(ns, dtype=torch.int64, device=gpu)
+    b.check(bad, 0)
+    torch.cuda.synchronize()
+    assert bool((bad == -1).all())
+    rng = np.random.default_rng(k * rows)
+    flips = {}
+    for s in range(0, ns, 2):
+        which = int(rng.integers(0, k + rows))
+        col = int(rng.integers(0, n))
+        flips[s] = (which, col)
+        t = data[s, which] if which < k else coding[s, which - k]
+        t[col] ^= 0x40
+    b.check(bad, 0)
+    torch.cuda.synchronize()
+    h_data, h_cod = _host(data), _host(coding)
+    want = _oracle_encode_all(oracle, coef, k, rows, [[h_data[s, j] for j in range(k)] for s in range(ns)])
+    got = _host(bad)
+    for s in range(ns):
+        mism = np.stack([h_cod[s, l] != want[s][l] for l in range(rows)])
+        if not mism.any():
+            assert got[s] == -1, s
+            continue
+        col = int(np.nonzero(mism.any(axis=0))[0][0])
+        row = int(np.nonzero(mism[:, col])[0][0])
+        assert int(got[s]) == (col << 8) | row, (s, flips.get(s), hex(int(got[s])), col, row)
+    b.close()

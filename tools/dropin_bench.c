@@ -3,7 +3,14 @@
  * device-resident shards (the way the reference's API is driven: one call
  * per stripe, erasure_code/erasure_code_perf.c:126-132), from T threads.
  *
- * usage: dropin_bench K P LEN STRIPES THREADS SECONDS [CALLS_PER_THREAD]
+ * usage: dropin_bench K P LEN STRIPES THREADS SECONDS [CALLS_PER_THREAD [OP]]
+ *
+ * OP (default encode): the synchronous call per stripe — encode
+ * (ec_encode_data), or a raid.h call over K sources: pq_gen / pq_check (P = 2
+ * rows: P, Q) or xor_gen / xor_check (P = 1), e.g. the reference harness
+ * raid/pq_gen_perf.c drives pq_gen the same way (one call per stripe). The
+ * check ops run on consistent stripes (every call must return 0) and finish
+ * with one corrupted byte that must be reported.
  *
  * STRIPES stripes of K + P shards live in HBM (one hipMalloc, shard s*(K+P)+i
  * at offset ((s*(K+P)+i) * LEN)); thread t encodes stripes t, t+T, ... in a
@@ -29,6 +36,12 @@
 #include <time.h>
 
 #include "erasure_code.h"
+#include "raid.h"
+
+enum { OP_ENCODE, OP_PQ_GEN, OP_XOR_GEN, OP_PQ_CHECK, OP_XOR_CHECK };
+static const char *const op_names[] = {"encode", "pq_gen", "xor_gen", "pq_check", "xor_check", NULL};
+static int g_op = OP_ENCODE;
+static long long g_check_fail;
 
 static double
 now(void)
@@ -60,16 +73,37 @@ shard(const worker_t *w, int s, int i)
         return w->base + ((size_t) s * (size_t) (w->k + w->p) + (size_t) i) * (size_t) w->len;
 }
 
+/* one call of the selected op on stripe s; returns its return value (0 for
+ * ec_encode_data) */
+static int
+call_op(const worker_t *w, int s)
+{
+        unsigned char *data[256], *coding[256];
+        void *arr[257];
+        int i;
+        if (g_op == OP_ENCODE) {
+                for (i = 0; i < w->k; i++)
+                        data[i] = shard(w, s, i);
+                for (i = 0; i < w->p; i++)
+                        coding[i] = shard(w, s, w->k + i);
+                ec_encode_data(w->len, w->k, w->p, w->tbls, data, coding);
+                return 0;
+        }
+        for (i = 0; i < w->k + w->p; i++)
+                arr[i] = shard(w, s, i);
+        switch (g_op) {
+        case OP_PQ_GEN: return pq_gen(w->k + 2, w->len, arr);
+        case OP_XOR_GEN: return xor_gen(w->k + 1, w->len, arr);
+        case OP_PQ_CHECK: return pq_check(w->k + 2, w->len, arr);
+        default: return xor_check(w->k + 1, w->len, arr);
+        }
+}
+
 static void
 encode_one(worker_t *w, int *s)
 {
-        unsigned char *data[256], *coding[256];
-        int i;
-        for (i = 0; i < w->k; i++)
-                data[i] = shard(w, *s, i);
-        for (i = 0; i < w->p; i++)
-                coding[i] = shard(w, *s, w->k + i);
-        ec_encode_data(w->len, w->k, w->p, w->tbls, data, coding);
+        if (call_op(w, *s) != 0)
+                __atomic_add_fetch(&g_check_fail, 1, __ATOMIC_RELAXED);
         *s += w->nthreads;
         if (*s >= w->stripes)
                 *s = w->t % w->stripes;
@@ -161,6 +195,17 @@ main(int argc, char **argv)
         seconds = atof(argv[6]);
         if (argc > 7)
                 fixed = atoll(argv[7]);
+        if (argc > 8) {
+                for (i = 0; op_names[i] && strcmp(op_names[i], argv[8]); i++)
+                        ;
+                if (!op_names[i]) {
+                        fprintf(stderr, "dropin_bench: unknown op %s\n", argv[8]);
+                        return 2;
+                }
+                g_op = i;
+                if (g_op != OP_ENCODE)
+                        p = g_op == OP_PQ_GEN || g_op == OP_PQ_CHECK ? 2 : 1;
+        }
         if (k < 1 || p < 1 || k + p > 255 || len < 1 || stripes < 1 || nthreads < 1 || nthreads > 256) {
                 fprintf(stderr, "dropin_bench: bad arguments\n");
                 return 2;
@@ -202,7 +247,31 @@ main(int argc, char **argv)
         if (!a || !tbls || !w || !th)
                 return 1;
         gf_gen_rs_matrix(a, k + p, k);
+        if (g_op != OP_ENCODE) {
+                /* the RAID rows: P = all ones, Q = 2^j (raid_base.c:44-68) */
+                unsigned char q = 1;
+                for (i = 0; i < k; i++) {
+                        a[(size_t) k * k + i] = 1;
+                        if (p == 2) {
+                                a[(size_t) (k + 1) * k + i] = q;
+                                q = gf_mul(q, 2);
+                        }
+                }
+        }
         ec_init_tables(k, p, a + (size_t) k * k, tbls);
+        if (g_op == OP_PQ_CHECK || g_op == OP_XOR_CHECK) {
+                /* consistent parity first: the timed checks must all pass */
+                const int gen = g_op;
+                worker_t g0 = {.t = 0, .nthreads = 1, .k = k, .p = p, .len = len, .stripes = stripes,
+                               .base = base, .tbls = tbls};
+                g_op = gen == OP_PQ_CHECK ? OP_PQ_GEN : OP_XOR_GEN;
+                for (i = 0; i < stripes; i++)
+                        if (call_op(&g0, i) != 0) {
+                                fprintf(stderr, "dropin_bench: parity generation failed\n");
+                                return 1;
+                        }
+                g_op = gen;
+        }
 
         for (i = 0; i < nthreads; i++) {
                 w[i] = (worker_t){.t = i, .nthreads = nthreads, .k = k, .p = p, .len = len,
@@ -221,11 +290,26 @@ main(int argc, char **argv)
                 calls += w[i].calls;
         }
         wall = now() - t0;
-        ok = check_stripe(&w[0], a, 0) == 0 && check_stripe(&w[0], a, stripes - 1) == 0;
-        printf("{\"k\": %d, \"p\": %d, \"len\": %d, \"stripes\": %d, \"threads\": %d, \"calls\": %lld, "
+        ok = check_stripe(&w[0], a, 0) == 0 && check_stripe(&w[0], a, stripes - 1) == 0 && g_check_fail == 0;
+        if (g_check_fail)
+                fprintf(stderr, "dropin_bench: %lld calls returned non-zero\n", g_check_fail);
+        if (ok && (g_op == OP_PQ_CHECK || g_op == OP_XOR_CHECK)) {
+                /* one corrupted byte in the middle of source 1 of stripe 0 must be reported */
+                unsigned char *b = shard(&w[0], 0, 1) + len / 2, v;
+                (void) hipMemcpy(&v, b, 1, hipMemcpyDeviceToHost);
+                v ^= 0x08;
+                (void) hipMemcpy(b, &v, 1, hipMemcpyHostToDevice);
+                if (call_op(&w[0], 0) == 0) {
+                        fprintf(stderr, "dropin_bench: corrupted stripe not reported\n");
+                        ok = 0;
+                }
+                v ^= 0x08;
+                (void) hipMemcpy(b, &v, 1, hipMemcpyHostToDevice);
+        }
+        printf("{\"op\": \"%s\", \"k\": %d, \"p\": %d, \"len\": %d, \"stripes\": %d, \"threads\": %d, \"calls\": %lld, "
                "\"wall_s\": %.4f, \"us_per_call\": %.2f, \"calls_per_s\": %.1f, \"gib_s\": %.3f, "
                "\"first_timed_call_us_thread0\": %.1f, \"self_check\": %s}\n",
-               k, p, len, stripes, nthreads, calls, wall, wall / ((double) calls / nthreads) * 1e6,
+               op_names[g_op], k, p, len, stripes, nthreads, calls, wall, wall / ((double) calls / nthreads) * 1e6,
                (double) calls / wall, (double) calls * (double) (k + p) * (double) len / wall / (double) (1 << 30),
                w[0].first_call_us, ok ? "true" : "false");
         (void) hipFree(base);
