@@ -70,7 +70,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads / pinned processes for the CPU baselines; 0 = one per physical "
-                         "core of this process's affinity set (SURVEY.md §8(d))")
+                         "core this process may use: its affinity set capped by its cgroup CPU quota "
+                         "(SURVEY.md §8(d))")
     ap.add_argument("--cold-ring", type=int, default=8,
                     help="distinct stripes each thread of the cold-cache SIMD-port baseline cycles over")
     ap.add_argument("--total-stripes", type=int, default=0,
@@ -240,42 +241,31 @@ def timed_steps(d: Dist, step, sync, steps: int, warmup: int):
     return d.max(t1 - t0)
 
 
-def enc_order() -> int:
-    """Work order the engine's vector encode launches with (ec_kernels.hip:enc_order):
-    2 = XCD-contiguous (default), 0 = tile-fastest (ISAL_HIP_ENC_ORDER=0)."""
-    return 0 if os.environ.get("ISAL_HIP_ENC_ORDER") == "0" else 2
-
-
 def enc_kernel(rows: int, k: int, coef) -> str:
     """The vector encode kernel the library launches for one pass of `rows`
-    (<= 8) outputs with coefficient matrix coef (rows x k): its load group
-    (enc_group), work order (enc_order) and variant — bit 0 the XOR path for
-    0/1 rows and columns (isal_hip_enc_masks: row 0 and column 0 hold only
-    0/1, k <= 64; ISAL_HIP_ENC_XOR=0 off), bit 1 low table halves from LDS
-    (more than 4 looked-up rows in passes of up to 6 rows, or of 7-8 rows
-    loading in groups of 5; ISAL_HIP_ENC_LDS=1 always, =0 never); both only in
-    the default order-2 policy. The library names the same instantiation on
-    stderr with ISAL_HIP_LOG=2."""
+    (<= 8) outputs with coefficient matrix coef (rows x k): variant bit 0 the
+    XOR path for 0/1 rows and columns (isal_hip_enc_masks: row 0 and column 0
+    hold only 0/1, k <= 64; ISAL_HIP_ENC_XOR=0 off), bit 1 low table halves
+    from LDS (more than 4 looked-up rows in passes of up to 6 rows, or of 7-8
+    rows loading in groups of 5; ISAL_HIP_ENC_LDS=1 always, =0 never); passes
+    of 5-8 rows stage their sources through the LDS-DMA ring (ec_encode_glds,
+    4 slots per wave, table halves from LDS; ISAL_HIP_ENC_GLDS=0 off). The
+    library names the same instantiation on stderr with ISAL_HIP_LOG=2."""
     import numpy as np
 
     c = np.asarray(coef, dtype=np.uint8).reshape(rows, k)
-    order = enc_order()
     fl = 0
-    if order == 2 and os.environ.get("ISAL_HIP_ENC_STORE") != "1":
-        if (os.environ.get("ISAL_HIP_ENC_XOR") != "0" and k <= 64 and int(c[0].max()) <= 1
-                and int(c[:, 0].max()) <= 1):
-            fl |= 1
-        lds = os.environ.get("ISAL_HIP_ENC_LDS")
-        wide5 = os.environ.get("ISAL_HIP_ENC_WIDE5") != "0"
-        if lds == "1" or (lds != "0" and rows - (fl & 1) > 4
-                          and (rows <= 6 or (enc_group(k, rows) == 5 and wide5))):  # ec_kernels.hip enc_lds
-            fl |= 2
-    if order == 2:
-        ld, st = 2, (3 if os.environ.get("ISAL_HIP_ENC_STORE") == "1" else 2)
-    else:
-        ld, st = 2, 2  # EncNT<U> = EncPol<U>: nt buffer loads and stores, tile-fastest
+    if os.environ.get("ISAL_HIP_ENC_XOR") != "0" and k <= 64 and int(c[0].max()) <= 1 and int(c[:, 0].max()) <= 1:
+        fl |= 1
+    if rows >= 5 and os.environ.get("ISAL_HIP_ENC_GLDS") != "0":
+        return f"ec_encode_glds<{rows}, 4, {fl | 2}>"  # ec_kernels.hip enc_glds
+    lds = os.environ.get("ISAL_HIP_ENC_LDS")
+    wide5 = os.environ.get("ISAL_HIP_ENC_WIDE5") != "0"
+    if lds == "1" or (lds != "0" and rows - (fl & 1) > 4
+                      and (rows <= 6 or (enc_group(k, rows) == 5 and wide5))):  # ec_kernels.hip enc_lds
+        fl |= 2
     # rocprofv3 prints every template argument, the variant's default 0 too
-    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, {ld}, {st}, {order}>, {fl}>"
+    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, 2, 2, 2>, {fl}>"
 
 
 def copy_ceiling(dev, nbytes: int = 2 << 30, reps: int = 10) -> dict:
@@ -728,7 +718,7 @@ def ref_harness_baseline(workload, k, p, n, procs):
                   f"AVX-512/GFNI kernels cannot be assembled)",
         "single_core_gib_s": gib(per_core),
         "host": {a: host.get(a) for a in ("model", "sockets", "physical_cores", "affinity_physical_cores",
-                                          "cgroup_cpu_quota", "cpus", "isa", "nasm")},
+                                          "cgroup_cpu_quota", "usable_cores", "cpus", "isa", "nasm")},
     }
     return res
 
@@ -1047,56 +1037,36 @@ def main(argv=None):
             crc_out = torch.zeros(S * (k + p), dtype=torch.int32, device=dev)
             bytes_per_launch = (k + p) * n * S
             if args.workload == "encode-crc":
-                u = enc_group(k)  # one load group (k == U): source CRC chains in registers
-                reg = k == u and os.environ.get("ISAL_HIP_CRC_SRC_CHAIN") == "reg"
-                x0 = "false" if reg else "true"  # Vandermonde row 0 derived (LDS-chain variant)
-                nb = 0 if reg or os.environ.get("ISAL_HIP_CRC_BYTE_DWORDS") == "0" else 4  # byte tables
+                u = next((g for g in (12, 10, 8, 6, 5, 4) if k >= g and k % g == 0), 4)  # enc_group_crc
                 # lane groups per workgroup: the launcher's rule (crc_kernels.hip fused_nv32)
                 tabs_b, la_b, cap = 32 * 256 * 4, k * 256 * 4, 160 * 1024
-                nv_env = os.environ.get("ISAL_HIP_CRC_FUSED_NV")
-                if not nb or tabs_b + 2 * la_b >= cap:
-                    nv = 1
-                elif nv_env in ("1", "2"):
-                    nv = int(nv_env)
-                else:
-                    nv = 2 if 2 * (cap // (tabs_b + 2 * la_b)) > cap // (tabs_b + la_b) else 1
-                kernel = (f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, {str(reg).lower()}, true, {x0}, "
-                          f"{nb}, {nv}>")
+                nv = 1 if tabs_b + 2 * la_b >= cap else (2 if 2 * (cap // (tabs_b + 2 * la_b)) > cap // (tabs_b + la_b)
+                                                         else 1)
+                # <P, FusedPol<U>, REG, SRC, X0 (Vandermonde row 0 derived), NB (byte tables), NV>
+                kernel = f"ec_encode_crc_v16<{p}, EncPol<{u}, 1, 1, 0>, false, true, true, 4, {nv}>"
                 workload = (f"C2 encode + CRC32C (crc32_iscsi) of all k+p shards in one pass: k={k} "
                             f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
             else:
                 batch.encode(torch.cuda.current_stream(dev).cuda_stream)
-                # pre-shifted chains by default, chain-step kernel under ISAL_HIP_CRC_PRE=0
-                m32 = 4 if os.environ.get("ISAL_HIP_CRC_STEP") == "4" else 1
-                kernel = (f"crc32c_shards<true, {m32}>" if os.environ.get("ISAL_HIP_CRC_PRE") == "0"
-                          else "crc32c_shards_pre")
+                kernel = "crc32c_shards_pre"  # pre-shifted chains, field tables
                 workload = (f"CRC32C (crc32_iscsi) of all k+p={k + p} shards, {n} B x {S} "
                             f"stripes/GPU, device-resident")
         elif args.workload == "encode-crc64":
             # encode + CRC64 (crc64_ecma_refl) of all k+p shards in one pass
             crc_out = torch.zeros(S * (k + p), dtype=torch.int64, device=dev)
             bytes_per_launch = (k + p) * n * S
-            u = enc_group(k)
-            reg = k == u and os.environ.get("ISAL_HIP_CRC64_SRC_CHAIN") == "reg"
-            # chunk path: 0 field tables, 1 slicing-by-8 byte tables, 2 hybrid byte/field
-            # tables (experiment), 3 byte tables pipelined into the GF rows (default;
-            # 2 and 3 for load group 10 only, 3 for p <= 4; elsewhere 1)
-            sl = {"0": 0, "1": 1, "2": 2}.get(os.environ.get("ISAL_HIP_CRC64_SLICE", "3"), 3)
-            if sl in (2, 3) and (u != 10 or reg or (sl == 3 and p > 4)):
-                sl = 1
-            # lane groups per workgroup: the launcher's rule (crc64_kernels.hip fused_nv)
-            tabs_b, la_b, cap = {0: 2688, 1: 4096, 2: 1024, 3: 4096}[sl] * 8, k * 256 * 8, 160 * 1024
-            nv_env = os.environ.get("ISAL_HIP_CRC64_FUSED_NV")
-            if reg or tabs_b + 2 * la_b >= cap:
-                nv = 1
-            elif nv_env in ("1", "2"):
-                nv = int(nv_env)
-            elif sl == 3:
-                nv = 1
+            u = next((g for g in (12, 10, 8, 6, 5, 4) if k >= g and k % g == 0), 4)  # group_u
+            # chunk path: 3 = byte tables pipelined into the GF rows (load group 10,
+            # p <= 4, one lane group), else 1 = byte tables after each pair, lane
+            # groups by the launcher's rule (crc64_kernels.hip fused_nv)
+            if u == 10 and p <= 4:
+                sl, nv = 3, 1
             else:
-                nv = 2 if 2 * (cap // (tabs_b + 2 * la_b)) > cap // (tabs_b + la_b) else 1
-            # X0: Vandermonde row 0 derived
-            kernel = f"ec_encode_crc64_v16<{p}, {u}, {str(reg).lower()}, true, {sl}, {nv}>"
+                tabs_b, la_b, cap = 4096 * 8, k * 256 * 8, 160 * 1024
+                sl = 1
+                nv = 1 if tabs_b + 2 * la_b >= cap else (2 if 2 * (cap // (tabs_b + 2 * la_b)) > cap // (tabs_b + la_b)
+                                                         else 1)
+            kernel = f"ec_encode_crc64_v16<{p}, {u}, true, {sl}, {nv}>"  # <P, U, X0 (row 0 derived), SL, NV>
             workload = (f"C2 encode + CRC64 (crc64_ecma_refl) of all k+p shards in one pass: k={k} "
                         f"p={p} Vandermonde RS, {n} B shards x {S} stripes/GPU")
         elif args.workload == "crc64":
@@ -1104,13 +1074,7 @@ def main(argv=None):
             crc_out = torch.zeros(S * (k + p), dtype=torch.int64, device=dev)
             bytes_per_launch = (k + p) * n * S
             batch.encode(torch.cuda.current_stream(dev).cuda_stream)
-            b8 = 8 if os.environ.get("ISAL_HIP_CRC64_BATCH") == "8" else 4
-            if os.environ.get("ISAL_HIP_CRC_PRE") == "0":
-                m = {"1": 1, "4": 4}.get(os.environ.get("ISAL_HIP_CRC64_STEP", ""), 2)
-                kernel = f"crc64_shards<true, {m}, {b8}>"
-            else:
-                pp = str(os.environ.get("ISAL_HIP_CRC64_PRE_PIPE") == "1").lower()
-                kernel = f"crc64_shards_pre<{b8}, {pp}>"
+            kernel = "crc64_shards_pre"  # pre-shifted chains, field tables
             workload = (f"CRC64 (crc64_ecma_refl) of all k+p={k + p} shards, {n} B x {S} "
                         f"stripes/GPU, device-resident")
         elif args.workload in RAID_ROWS:
@@ -1303,8 +1267,9 @@ def main(argv=None):
         import cpu_ref_baseline as crb
 
         # one pinned process (or thread) per physical core
-        # this process may use; the count is recorded in each baseline
-        threads = args.cpu_threads or len(crb.physical_cpus())
+        # this process may use (its affinity set, capped by its cgroup CPU
+        # quota); the count is recorded in each baseline
+        threads = args.cpu_threads or crb.usable_cores()
         if args.workload in ("encode", "decode", "update"):
             # the reference's own perf harness (erasure_code_perf.c /
             # erasure_code_update_perf.c) on this host's cores

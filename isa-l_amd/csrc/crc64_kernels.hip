@@ -142,45 +142,23 @@ __device__ __forceinline__ void load_lds(uint64_t* dst, const uint64_t* __restri
   for (int i = threadIdx.x; i < N / 2; i += kBlock * NV) d[i] = s[i];
 }
 
-[[maybe_unused]] constexpr int kBatch = 4;  // full tiles whose loads are issued together (default)
 constexpr int kCE = ISAL_HIP_CRC64_CHUNK_ENTRIES;
 
 #ifndef ISAL_FUSED64_PART  // standalone kernels: the main object only
 
-// LDS layout of crc64_shards<VEC, M>: chunk map (m = 0) and Z^4096 [kKernTab],
-// the chunk maps followed by m = 1..M-1 tiles, Z^(4096*M).
-template <int M>
-constexpr int shards_lds() {
-  return kKernTab + (M > 1 ? (M - 1) * kCE + kOp : 0);
-}
-template <int M>
-__device__ __forceinline__ const uint64_t* chunk_map(const uint64_t* lt, int m) {
-  return m == 0 ? lt + kChunk : lt + kKernTab + (m - 1) * kCE;
-}
-
-// Chains of the full tiles. Item = (stripe, shard, block), shard-major within
-// a stripe: part index = ((stripe * nsh + i) * nblk + blk) * 256 + L.
-// M > 1 advances the chain M tiles per step,
-//   a = Z^(4096*M)(a) ^ XOR_h (Z^(4096*(M-1-h)) o raw(0, .))(chunk_h),
-// with the shifted chunk maps precomputed: 14 + 28*M lookups per M tiles
-// instead of 42*M (M = 4: -25 %).
-template <bool VEC, int M, int B = kBatch>
-__global__ __launch_bounds__(kBlock) void crc64_shards(const uint64_t* __restrict__ ptrs,
-                                                       int ptr_stride, int nsh, int len,
-                                                       unsigned nitems, unsigned nblk, unsigned tt,
-                                                       unsigned nfull,
-                                                       const uint64_t* __restrict__ tabs,
-                                                       uint64_t* __restrict__ part) {
-  static_assert(B % M == 0, "chain step divides the load batch");
-  __shared__ uint64_t lt[shards_lds<M>()];
+// Shards that are not 16-byte aligned: byte loads, one Z^4096 chain step per
+// tile. Item = (stripe, shard, block), shard-major within a stripe: part index
+// = ((stripe * nsh + i) * nblk + blk) * 256 + L. (Chain steps of 2 and 4
+// tiles through shifted chunk maps for aligned shards — ISAL_HIP_CRC64_STEP,
+// _BATCH — were superseded by crc64_shards_pre and removed in round 5.)
+__global__ __launch_bounds__(kBlock) void crc64_shards_bytes(const uint64_t* __restrict__ ptrs, int ptr_stride,
+                                                             int nsh, int len, unsigned nitems, unsigned nblk,
+                                                             unsigned tt, unsigned nfull,
+                                                             const uint64_t* __restrict__ tabs,
+                                                             uint64_t* __restrict__ part) {
+  __shared__ uint64_t lt[kKernTab];
   load_lds<kKernTab>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
-  if constexpr (M > 1) {
-    load_lds<(M - 1) * kCE>(lt + kKernTab, tabs + ISAL_HIP_CRC64_CHUNKX_TAB);
-    load_lds<kOp>(lt + kKernTab + (M - 1) * kCE,
-                  tabs + ISAL_HIP_CRC64_SHIFTX_TAB + (M == 4 ? kOp : 0));
-  }
   __syncthreads();
-  const uint64_t* shift_m = M > 1 ? lt + kKernTab + (M - 1) * kCE : lt + kShift;
   const long long lane = threadIdx.x * kVec;
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned si = w / nblk, blk = w - si * nblk;
@@ -188,94 +166,34 @@ __global__ __launch_bounds__(kBlock) void crc64_shards(const uint64_t* __restric
     const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
     const unsigned t0 = blk * tt, t1 = t0 + tt < nfull ? t0 + tt : nfull;
     uint64_t a = 0;
-    unsigned t = t0;
-    if constexpr (VEC) {
-      for (; t + B <= t1; t += B) {
-        uint4 x[B];
-#pragma unroll
-        for (unsigned g = 0; g < B; ++g)
-          x[g] = load16<kBufNT>(base, static_cast<long long>(t + g) * kTile + lane, len);
-#pragma unroll
-        for (unsigned g = 0; g < B; g += M) {
-          X64 c{0u, 0u};
-#pragma unroll
-          for (int h = 0; h < M; ++h)
-            chunk_acc(c, chunk_map<M>(lt, M - 1 - h), x[g + h].x, x[g + h].y, x[g + h].z,
-                      x[g + h].w);
-          apply_op_acc(c, shift_m, a);
-          a = c.get();
-        }
-      }
-      for (; t < t1; ++t) {
-        const uint4 x = load16<kBufNT>(base, static_cast<long long>(t) * kTile + lane, len);
-        X64 c{0u, 0u};
-        chunk_acc(c, lt + kChunk, x.x, x.y, x.z, x.w);
-        apply_op_acc(c, lt + kShift, a);
-        a = c.get();
-      }
-    } else {
-      for (; t < t1; ++t)
-        a = apply_op(lt + kShift, a) ^
-            chunk_crc_bytes(lt + kChunk, base, static_cast<long long>(t) * kTile + lane);
-    }
+    for (unsigned t = t0; t < t1; ++t)
+      a = apply_op(lt + kShift, a) ^ chunk_crc_bytes(lt + kChunk, base, static_cast<long long>(t) * kTile + lane);
     part[static_cast<size_t>(w) * kBlock + threadIdx.x] = a;
   }
 }
 
-// Pre-shifted chains (the fused kernel's idea, crc64_kernels.hip SL path) on
-// conflict-free 5-bit field tables: a lane keeps b = Z^4080_u(a) in the
-// u-domain, XORs it into the next chunk's first 8 bytes like a CRC register and
-// maps the chunk once, b' = F'_u(chunk ^ b) — 28 lookups per tile and no chain
-// step (M = 2 spends 35) — the item's last tile applies F_u and leaves the
-// plain chain. Loads are double-buffered (the next B tiles in flight).
-//
-// PIPE (ISAL_HIP_CRC64_PRE_PIPE=1, a measured negative result, see pre_pipe()):
-// the compiler emits chunk_acc as pairs of ds_read_b64 with an
-// s_waitcnt after every pair, so a tile is 14 dependent LDS round trips. Only
-// the first 8 bytes' 14 lookups depend on the chain; the last 8 bytes' do not.
-// The pipelined form issues a tile's 14 chain-dependent lookups, folds the
-// independent 14 issued one tile earlier, issues the next tile's independent
-// 14, then folds the dependent ones: one LDS round trip per tile on the chain.
-// Volatile LDS loads + scheduling barriers keep the issue order (as in the
-// fused kernel's SL 3 stages). Same tables and arithmetic.
-struct Look14 {
-  uint64_t v[14];
-};
+// Pre-shifted chains (the fused kernel's idea) on conflict-free 5-bit field
+// tables: a lane keeps b = Z^4080_u(a) in the u-domain, XORs it into the next
+// chunk's first 8 bytes like a CRC register and maps the chunk once, b' =
+// F'_u(chunk ^ b) — 28 lookups per tile and no chain step — the item's last
+// tile applies F_u and leaves the plain chain. Loads are double-buffered (the
+// next B tiles in flight). (A form with the lookups software-pipelined,
+// ISAL_HIP_CRC64_PRE_PIPE=1, ran 2.94-2.95 vs 2.82-2.85 ms on C2 — 56 lookup
+// VGPRs in flight cut the occupancy from 7 to 3 waves per SIMD —
+// profiles/r03/r03_crc64_prepipe_benches.jsonl; removed in round 5, as was a
+// batch of 8 tiles, ISAL_HIP_CRC64_BATCH=8, measured slower.)
+constexpr int kPreBatch = 4;
 
-__device__ __forceinline__ uint64_t tab_issue(const uint64_t* t, int f, uint32_t o) {
-  typedef const __attribute__((address_space(3))) char lchar;
-  typedef const volatile __attribute__((address_space(3))) uint64_t lu64;
-  return *(lu64*)((lchar*)(t) + f * 256 + o);
-}
-
-// Issue the 14 field lookups of (w0, w1) in the 14 tables at t.
-__device__ __forceinline__ void issue14(Look14& r, const uint64_t* t, uint32_t w0, uint32_t w1) {
-  uint32_t o[kF], q[kF];
-  field_offsets8(w0, o);
-  field_offsets8(w1, q);
-#pragma unroll
-  for (int f = 0; f < kF; ++f) r.v[f] = tab_issue(t, f, o[f]);
-#pragma unroll
-  for (int f = 0; f < kF; ++f) r.v[kF + f] = tab_issue(t, kF + f, q[f]);
-}
-
-__device__ __forceinline__ void fold14(X64& acc, const Look14& r) {
-#pragma unroll
-  for (int i = 0; i < 14; i += 2) acc.add2(r.v[i], r.v[i + 1]);
-}
-
-template <int B, bool PIPE = true>
-__global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __restrict__ ptrs,
-                                                           int ptr_stride, int nsh, int len,
-                                                           unsigned nitems, unsigned nblk,
+__global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __restrict__ ptrs, int ptr_stride,
+                                                           int nsh, int len, unsigned nitems, unsigned nblk,
                                                            unsigned tt, unsigned nfull, int uswap,
                                                            const uint64_t* __restrict__ tabs,
-                                                           uint64_t* __restrict__ part, int xcd) {
+                                                           uint64_t* __restrict__ part) {
+  constexpr int B = kPreBatch;
   __shared__ uint64_t lt[2 * kCE];  // F_u, F'_u
   load_lds<2 * kCE>(lt, tabs + ISAL_HIP_CRC64_PRE_TAB);
   __syncthreads();
   const long long lane = threadIdx.x * kVec;
-  constexpr int D2 = 2 * kF * 32;  // tables of the chunk's last 8 bytes
   auto step = [&](unsigned t, unsigned t1, X64 b, const uint4& x) __attribute__((always_inline)) {
     X64 c{0u, 0u};
     if (t + 1 == t1)
@@ -284,28 +202,7 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
       chunk_acc(c, lt + kCE, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
     return c;
   };
-  // B tiles with the lookups pipelined (PIPE). LAST: the batch ends the item,
-  // so its last tile uses F_u (a compile-time table base keeps every lookup's
-  // table offset in the ds_read immediate).
-  auto batch = [&](auto last_c, X64 b, const uint4 (&x)[B]) __attribute__((always_inline)) {
-    constexpr bool LAST = decltype(last_c)::value;
-    Look14 ind, dep;
-    issue14(ind, (LAST && B == 1 ? lt : lt + kCE) + D2, x[0].z, x[0].w);
-#pragma unroll
-    for (int g = 0; g < B; ++g) {
-      issue14(dep, LAST && g + 1 == B ? lt : lt + kCE, x[g].x ^ b.lo, x[g].y ^ b.hi);
-      __builtin_amdgcn_sched_barrier(0);
-      X64 c{0u, 0u};
-      fold14(c, ind);
-      if (g + 1 < B) issue14(ind, (LAST && g + 2 == B ? lt : lt + kCE) + D2, x[g + 1].z, x[g + 1].w);
-      __builtin_amdgcn_sched_barrier(0);
-      fold14(c, dep);
-      b = c;
-    }
-    return b;
-  };
-  for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
-    const unsigned w = xcd_item(ww, nitems, xcd);
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned si = w / nblk, blk = w - si * nblk;
     const unsigned stripe = si / nsh, i = si - stripe * nsh;
     const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
@@ -326,15 +223,8 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
         for (int g = 0; g < B; ++g)
           xn[g] = load16<kBufNT>(base, static_cast<long long>(t + B + g) * kTile + lane, len);
       }
-      if constexpr (PIPE) {
-        if (t + B == t1)
-          b = batch(std::true_type{}, b, x);
-        else
-          b = batch(std::false_type{}, b, x);
-      } else {
 #pragma unroll
-        for (int g = 0; g < B; ++g) b = step(t + g, t1, b, x[g]);
-      }
+      for (int g = 0; g < B; ++g) b = step(t + g, t1, b, x[g]);
     }
     for (; t < t1; ++t)
       b = step(t, t1, b, load16<kBufNT>(base, static_cast<long long>(t) * kTile + lane, len));
@@ -415,36 +305,6 @@ __global__ __launch_bounds__(kBlock) void crc64_combine(
 
 constexpr unsigned long long kMaxItems = 1ull << 30;
 
-// Tiles per chain step of crc64_shards (ISAL_HIP_CRC64_STEP = 1, 2 or 4).
-// Measured on the C2 shape (profiles/r01/r01_crc64_step_sweep.txt): 2 tiles per
-// step with 4 loads in flight is fastest; 4 per step costs occupancy (LDS).
-int chain_step() {
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_STEP);
-  return v == 1 || v == 4 ? static_cast<int>(v) : 2;
-}
-
-// Pre-shifted chains in the standalone kernel (ISAL_HIP_CRC_PRE=0: the
-// chain-step kernels above, with ISAL_HIP_CRC64_STEP / _BATCH).
-bool shards_pre() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC_PRE) != 0;
-}
-
-// Pipelined lookups in the pre-shifted kernel (ISAL_HIP_CRC64_PRE_PIPE=1; off
-// by default). C2 shape, same box, two runs each
-// (profiles/r03/r03_crc64_prepipe_benches.jsonl, r03_pmc_sq_crc64_prepipe.txt):
-// 2.82-2.85 ms unpipelined vs 2.94-2.95 ms pipelined — SQ_WAIT_INST_LDS fell
-// 41 % but the 56 lookup VGPRs in flight cut the occupancy from 7 to 3 waves
-// per SIMD, and the kernel was not bound by its LDS round trips.
-bool pre_pipe() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_PRE_PIPE) == 1;
-}
-
-// Full tiles loaded per batch (ISAL_HIP_CRC64_BATCH = 4 or 8), in the
-// chain-step kernels and in the pre-shifted kernel's double buffer.
-int load_batch() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_BATCH) == 8 ? 8 : 4;
-}
-
 #else  // ISAL_FUSED64_PART: one object per parity-row count P (parallel build)
 
 // ---------------------------------------------------------------------------
@@ -457,8 +317,7 @@ int load_batch() {
 // layout (shards 0..k-1 = sources, k..k+P-1 = parity) and crc64_combine
 // finishes them, reading the ragged tail (len % 4096) straight from the
 // shards: the kernel's last block encodes that tile without checksumming it.
-// Source chains live in registers when the k sources form one load group
-// (REG: k == U, e.g. C2's k = 10), else in LDS (lane-private words).
+// Source chains live in LDS (lane-private words).
 // ---------------------------------------------------------------------------
 template <int P, int U, bool R0 = false, class Feed>
 __device__ __forceinline__ void mac_feed(uint32_t (&acc)[P][4], const uint4 (&x)[U], int j,
@@ -491,35 +350,25 @@ __device__ __forceinline__ void load_grp(uint4 (&x)[U], const uint64_t* __restri
   for (int u = 0; u < U; ++u) x[u] = load16<kNT>(sp[j + u], off, len);
 }
 
-// LDS layout of the fused kernel: chunk map, Z^4096 [kKernTab], then the chunk
-// map followed by one tile (T1) and Z^8192.
-constexpr int kT1 = kKernTab, kZ2 = kKernTab + kCE;
-
-// One chain step of phase PH (0 single, 1 even, 2 odd tile of a pair).
-template <int PH>
-__device__ __forceinline__ uint64_t chain_step(const uint64_t* lt, uint64_t a, uint32_t w0,
-                                               uint32_t w1, uint32_t w2, uint32_t w3) {
-  X64 c = PH == 2 ? x64(a) : X64{0u, 0u};
-  chunk_acc(c, lt + (PH == 1 ? kT1 : kChunk), w0, w1, w2, w3);
-  if constexpr (PH != 2) apply_op_acc(c, lt + (PH == 1 ? kZ2 : kShift), a);
-  return c.get();
-}
-
-// ---- slicing-by-8 chunk path of the fused kernel (SL) ----------------------
-// The field-table path costs ~1.7 VALU per 5-bit field offset + 1 per 64-bit
-// fold, 28 lookups per 16-byte chunk plus 7 per tile for the chain step, and
-// the fused kernel is VALU-issue-bound. Here, in the u-domain
-// (crc64_host.c: u = pi(s), one update rule u' = A(d ^ u) for every flavour),
-// a lane keeps its chain PRE-SHIFTED: b = Z^4080_u(a), the chain advanced by
-// the 4080 bytes of the other lanes' chunks that follow its own in the tile.
-// Then the next tile's raw value is raw_u(b, chunk) — b is XORed into the
-// chunk's first 8 bytes like a CRC register — and the step needs no separate
-// shift map at all:
+// ---- the fused kernel's chunk path: pre-shifted chains, byte tables --------
+// In the u-domain (crc64_host.c: u = pi(s), one update rule u' = A(d ^ u) for
+// every flavour) a lane keeps its chain PRE-SHIFTED: b = Z^4080_u(a), the
+// chain advanced by the 4080 bytes of the other lanes' chunks that follow its
+// own in the tile. Then the next tile's raw value is raw_u(b, chunk) — b is
+// XORed into the chunk's first 8 bytes like a CRC register — and the step
+// needs no separate shift map at all:
 //   u1 = A(lo8 ^ b),  b' = A'(hi8 ^ u1)   (A' = Z^4080_u o A)
 // and the block's last tile ends with A instead of A', leaving the plain
 // chain a. 16 byte-indexed lookups per chunk, each offset one SDWA shift
 // (byte select + << 3); the 256-entry tables are not bank-conflict-free (8
 // entries per bank pair): VALU issue traded for LDS cycles.
+//
+// Formulations measured and removed (profiles/r05/r05_fused_model.txt):
+// 5-bit field tables with a Z^4096 step per tile (ISAL_HIP_CRC64_SLICE=0, C2
+// 4.27 ms vs 3.21), hybrid 5+3-bit tables (SLICE=2, +10 %), pre-shifted 5-bit
+// field tables (SLICE=4, round 5: conflict-free but VALU-bound, 3.93 vs
+// 3.34 ms same box), source chains in registers (SRC_CHAIN=reg, 5 % slower)
+// and paired chain steps of the field path (FUSED_PAIR).
 constexpr int kSA = 0, kSB = 8 * 256;  // A, A' in LDS
 constexpr int kSlLds = 16 * 256;
 
@@ -560,80 +409,15 @@ __device__ __forceinline__ void slice8_acc(X64& acc, const uint64_t* t, uint32_t
   acc.add2(tab8_at(t, 6, q[2]), tab8_at(t, 7, q[3]));
 }
 
-// Hybrid tables (SL == 2, an LDS bank-conflict experiment): each byte b_j of
-// the 8-byte word splits into its high 5 bits — a 32-entry table H_j, one bank
-// row, conflict-free, offset (b_j & 0xF8) in one SDWA op — and its low 3 bits,
-// paired with its neighbour's into a 6-bit field of a 64-entry table G_q (two
-// rows, at most 2-way). 12 lookups per 8 bytes instead of 8, LDS 8 KiB
-// instead of 32 KiB; derived in LDS from the byte tables at kernel start
-// (A_j linear: A_j[v] = H_j[v >> 3] ^ A_j[v & 7]).
-constexpr int kHyG = 8 * 32;        // G tables after the 8 H tables (entries)
-constexpr int kHySet = kHyG + 4 * 64;  // one hybrid set (A or A')
-constexpr int kHyLds = 2 * kHySet;
-
-__device__ __forceinline__ void hybrid_tables(uint64_t* lt, const uint64_t* __restrict__ bytes,
-                                              int nthreads) {
-  for (int i = threadIdx.x; i < kHyLds; i += nthreads) {
-    const int set = i / kHySet, r = i % kHySet;
-    const uint64_t* a = bytes + set * (8 * 256);
-    uint64_t v;
-    if (r < kHyG) {
-      v = a[(r / 32) * 256 + ((r % 32) << 3)];
-    } else {
-      const int q = (r - kHyG) / 64, f = (r - kHyG) % 64;
-      v = a[(2 * q) * 256 + (f & 7)] ^ a[(2 * q + 1) * 256 + (f >> 3)];
-    }
-    lt[i] = v;
-  }
-}
-
-// acc ^= S(w) for one dword (bytes j0..j0+3 of the 8-byte word) through the
-// hybrid set at t: 4 H lookups + 2 G lookups, 9 VALU offset ops.
-template <int J0>
-__device__ __forceinline__ void hyb4_acc(X64& acc, const uint64_t* t, uint32_t w) {
-  const uint32_t m = 0xF8u;
-  uint32_t h[4];
-  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
-      : "=v"(h[0]) : "v"(m), "v"(w));
-  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
-      : "=v"(h[1]) : "v"(m), "v"(w));
-  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
-      : "=v"(h[2]) : "v"(m), "v"(w));
-  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
-      : "=v"(h[3]) : "v"(m), "v"(w));
-  // f byte 0 = lo3(b0) | lo3(b1) << 3, f byte 2 = lo3(b2) | lo3(b3) << 3
-  const uint32_t f = ((w >> 5) & 0x00380038u) | (w & 0x07070707u);
-  uint32_t g[2];
-  byte_offs8(f, g[0], g[1]);
-  const char* tc = reinterpret_cast<const char*>(t);
-  auto H = [&](int j, uint32_t o) { return *reinterpret_cast<const uint64_t*>(tc + (J0 + j) * 256 + o); };
-  auto G = [&](int q, uint32_t o) {
-    return *reinterpret_cast<const uint64_t*>(tc + kHyG * 8 + (J0 / 2 + q) * 512 + o);
-  };
-  acc.add2(H(0, h[0]), H(1, h[1]));
-  acc.add2(H(2, h[2]), H(3, h[3]));
-  acc.add2(G(0, g[0]), G(1, g[1]));
-}
-
-__device__ __forceinline__ void hyb8_acc(X64& acc, const uint64_t* t, uint32_t lo, uint32_t hi) {
-  hyb4_acc<0>(acc, t, lo);
-  hyb4_acc<4>(acc, t, hi);
-}
-
 // One tile of a pre-shifted u-domain chain b (phase 1: the block's last tile,
-// which returns the plain chain a instead). SL 1: byte tables, 2: hybrid.
-template <int PH, int SL = 1>
-__device__ __forceinline__ uint64_t chain_step_sl(const uint64_t* lt, uint64_t b, uint32_t w0,
-                                                  uint32_t w1, uint32_t w2, uint32_t w3) {
+// which returns the plain chain a instead).
+template <int PH>
+__device__ __forceinline__ uint64_t chain_step_sl(const uint64_t* lt, uint64_t b, uint32_t w0, uint32_t w1,
+                                                  uint32_t w2, uint32_t w3) {
   X64 u{0u, 0u};
   X64 c{0u, 0u};
-  if constexpr (SL == 2) {
-    hyb8_acc(u, lt, w0 ^ static_cast<uint32_t>(b), w1 ^ static_cast<uint32_t>(b >> 32));
-    hyb8_acc(c, lt + (PH == 1 ? 0 : kHySet), w2 ^ u.lo, w3 ^ u.hi);
-  } else {
-    slice8_acc(u, lt + kSA, w0 ^ static_cast<uint32_t>(b), w1 ^ static_cast<uint32_t>(b >> 32));
-    slice8_acc(c, lt + (PH == 1 ? kSA : kSB), w2 ^ u.lo, w3 ^ u.hi);
-  }
+  slice8_acc(u, lt + kSA, w0 ^ static_cast<uint32_t>(b), w1 ^ static_cast<uint32_t>(b >> 32));
+  slice8_acc(c, lt + (PH == 1 ? kSA : kSB), w2 ^ u.lo, w3 ^ u.hi);
   return c.get();
 }
 
@@ -650,7 +434,7 @@ __device__ __forceinline__ uint64_t chain_step_sl(const uint64_t* lt, uint64_t b
 //   row r1 | F1a fold, R2a: a's last 8 bytes
 //   row r2 | F2a fold -> a's state; R1b
 //   row r3 (+ any further rows) | F1b fold, R2b (finished by the next pair)
-// Same tables, same arithmetic as chain_step_sl<PH, 1>.
+// Same tables, same arithmetic as chain_step_sl<PH>.
 struct Look8 {
   uint64_t v[8];
 };
@@ -751,9 +535,9 @@ __device__ __forceinline__ void mac_feed_pipe(uint32_t (&acc)[P][4], const uint4
   *cp = fold8(car).get();
 }
 
-template <int P, int U, bool REG>
+template <int P, int U>
 constexpr int fused64_waves() {
-  constexpr int est = (4 * U * (REG ? 2 : 1) + 6 * P + (REG ? 2 * U : 0) + 88 + 7) / 8 * 8;
+  constexpr int est = (4 * U + 6 * P + 88 + 7) / 8 * 8;
   constexpr int w = 512 / est;
   return w > 8 ? 8 : (w < 2 ? 2 : w);
 }
@@ -763,139 +547,74 @@ constexpr int fused64_waves() {
 // chain is not computed per tile but formed once per block from those
 // sources' chains. A compile-time variant: a runtime row mask in the tile
 // loop costs registers.
-// SL: chunks through the slicing tables, chains in the u-domain; uswap (norm
-// flavours) turns them back into registers (u = bswap(s)) before they are stored.
+// SL 3: the chain steps pipelined into the GF rows (load group 10, P <= 4);
+// SL 1: the same steps after each source pair's GF work. Chains in the
+// u-domain; uswap (norm flavours) turns them back into registers (u =
+// bswap(s)) before they are stored.
 // NV: independent 256-lane groups per workgroup. They share one LDS copy of the
 // tables (each works its own items, no barrier after the table load), so the
 // per-lane source chains, not the tables, set how many waves fit a CU.
-template <int P, int U, bool REG, bool X0 = false, int SL = 0, int NV = 1>
-__global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_encode_crc64_v16(
+template <int P, int U, bool X0, int SL, int NV>
+__global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U>())) void ec_encode_crc64_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, const uint32_t* __restrict__ tbl, int len,
-    int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged, int pair,
-    unsigned long long x0src, int uswap, const uint64_t* __restrict__ tabs,
-    uint64_t* __restrict__ part, int xcd) {
-  __shared__ uint64_t lt[SL == 2 ? kHyLds : SL ? kSlLds : kKernTab + kCE + kOp];
-  extern __shared__ uint64_t la[];  // [k][kBlock * NV] source chains when !REG
-  if constexpr (SL == 2) {
-    hybrid_tables(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB, kBlock * NV);
-  } else if constexpr (SL) {
-    load_lds<kSlLds, NV>(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB);
-  } else {
-    load_lds<kKernTab, NV>(lt, tabs + ISAL_HIP_CRC64_CHUNK_TAB);
-    load_lds<kCE, NV>(lt + kT1, tabs + ISAL_HIP_CRC64_CHUNKX_TAB);
-    load_lds<kOp, NV>(lt + kZ2, tabs + ISAL_HIP_CRC64_SHIFTX_TAB);
-  }
+    int k, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, int ragged,
+    unsigned long long x0src, int uswap, const uint64_t* __restrict__ tabs, uint64_t* __restrict__ part) {
+  static_assert(SL == 1 || SL == 3, "byte-table chunk paths");
+  __shared__ uint64_t lt[kSlLds];
+  extern __shared__ uint64_t la[];  // [k][kBlock * NV] source chains
+  load_lds<kSlLds, NV>(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB);
   constexpr int kLa = kBlock * NV;           // source-chain row stride
   const unsigned tid = threadIdx.x % kBlock;  // lane within its group
   __syncthreads();
-  auto step = [&](auto phc, uint64_t a, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
-                  __attribute__((always_inline)) {
-    if constexpr (SL)
-      return chain_step_sl<decltype(phc)::value, SL>(lt, a, w0, w1, w2, w3);
-    else
-      return chain_step<decltype(phc)::value>(lt, a, w0, w1, w2, w3);
-  };
-  auto to_reg = [&](uint64_t v) __attribute__((always_inline)) {
-    return SL && uswap ? __builtin_bswap64(v) : v;
-  };
+  auto to_reg = [&](uint64_t v) __attribute__((always_inline)) { return uswap ? __builtin_bswap64(v) : v; };
   const int nsh = k + P;
   const long long lane = tid * kVec;
-  for (unsigned ww = blockIdx.x * NV + threadIdx.x / kBlock; ww < nitems; ww += gridDim.x * NV) {
-    const unsigned w = xcd_item(ww, nitems, xcd, NV);
+  for (unsigned w = blockIdx.x * NV + threadIdx.x / kBlock; w < nitems; w += gridDim.x * NV) {
     const unsigned stripe = w / nblk, blk = w - stripe * nblk;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const unsigned t0 = blk * tt, t1 = t0 + tt < nfull ? t0 + tt : nfull;
-    uint64_t ao[P], ra[REG ? U : 1];
+    uint64_t ao[P];
 #pragma unroll
     for (int l = 0; l < P; ++l) ao[l] = 0;
-#pragma unroll
-    for (int j = 0; j < (REG ? U : 1); ++j) ra[j] = 0;
-    if constexpr (!REG)
-      for (int j = 0; j < k; ++j) la[j * kLa + threadIdx.x] = 0;
-    // Chain phase of a tile (uniform across the workgroup, a template
-    // argument of the tile body). With pair, tiles go in pairs: the even tile
-    // applies a = Z^8192(a) ^ T1(chunk), the odd one a ^= raw(0, chunk) — 70
-    // lookups per two tiles instead of 84, no extra state; an unpaired tile
-    // takes the single step a = Z^4096(a) ^ raw(0, chunk).
-    // SL: phase 1 marks the block's last tile (it returns the plain chain).
-    auto phase_of = [&](unsigned t) __attribute__((always_inline)) {
-      if constexpr (SL)
-        return t + 1 == t1 ? 1 : 0;
-      else
-        return !pair ? 0 : ((t - t0) & 1) ? 2 : (t + 1 < t1 ? 1 : 0);
-    };
-    auto with_phase = [&](int ph, auto&& body) __attribute__((always_inline)) {
-      if (ph == 1)
+    for (int j = 0; j < k; ++j) la[j * kLa + threadIdx.x] = 0;
+    // phase 1 marks the block's last tile (it returns the plain chain)
+    auto with_phase = [&](bool last, auto&& body) __attribute__((always_inline)) {
+      if (last)
         body(std::integral_constant<int, 1>{});
-      else if (ph == 2)
-        body(std::integral_constant<int, 2>{});
       else
         body(std::integral_constant<int, 0>{});
     };
-    auto tile_body = [&](auto phc, uint32_t (&acc)[P][4], long long off, auto&& macs)
-                         __attribute__((always_inline)) {
-      auto feed = [&](int j, const uint4& x) __attribute__((always_inline)) {
-        if constexpr (REG) {
-          ra[j] = step(phc, ra[j], x.x, x.y, x.z, x.w);
-        } else {
+    for (unsigned t = t0; t < t1; ++t) {
+      const long long off = static_cast<long long>(t) * kTile + lane;
+      uint32_t acc[P][4] = {};
+      int z = 0;  // opaque zero: keeps the coefficient loads inside the loop
+      asm volatile("" : "+s"(z));
+      with_phase(t + 1 == t1, [&](auto phc) __attribute__((always_inline)) {
+        constexpr int PH = decltype(phc)::value;
+        auto feed = [&](int j, const uint4& x) __attribute__((always_inline)) {
           uint64_t* a = la + j * kLa + threadIdx.x;
-          *a = step(phc, *a, x.x, x.y, x.z, x.w);
+          *a = chain_step_sl<PH>(lt, *a, x.x, x.y, x.z, x.w);
+        };
+        int j = 0;
+        for (; j + U <= k; j += U) {
+          uint4 x[U];
+          load_grp<U>(x, sp, j, off, len);
+          if constexpr (SL == 3)
+            mac_feed_pipe<P, U, X0, PH>(acc, x, j, tbl + z, la + threadIdx.x, kLa, lt, x0src);
+          else
+            mac_feed<P, U, X0>(acc, x, j, tbl + z, feed, x0src);
         }
-      };
-      macs(feed);
+        for (; j < k; ++j) {
+          uint4 x[1];
+          load_grp<1>(x, sp, j, off, len);
+          mac_feed<P, 1, X0>(acc, x, j, tbl + z, feed, x0src);
+        }
 #pragma unroll
-      for (int l = 0; l < P; ++l) {
-        store16<kNT>(sp[k + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
-        if (!(X0 && l == 0))
-          ao[l] = step(phc, ao[l], acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
-      }
-    };
-    if constexpr (REG) {
-      // the next tile's sources are in flight while this tile's GF and CRC
-      // work runs (the lookups otherwise leave HBM idle)
-      uint4 xn[U];
-      if (t0 < t1) load_grp<U>(xn, sp, 0, static_cast<long long>(t0) * kTile + lane, len);
-      for (unsigned t = t0; t < t1; ++t) {
-        const long long off = static_cast<long long>(t) * kTile + lane;
-        uint4 x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = xn[u];
-        if (t + 1 < t1) load_grp<U>(xn, sp, 0, off + kTile, len);
-        uint32_t acc[P][4] = {};
-        int z = 0;  // opaque zero: keeps the coefficient loads inside the loop
-        asm volatile("" : "+s"(z));
-        with_phase(phase_of(t), [&](auto phc) __attribute__((always_inline)) {
-          tile_body(phc, acc, off, [&](auto& feed) __attribute__((always_inline)) {
-            mac_feed<P, U, X0>(acc, x, 0, tbl + z, feed, x0src);
-          });
-        });
-      }
-    } else {
-      for (unsigned t = t0; t < t1; ++t) {
-        const long long off = static_cast<long long>(t) * kTile + lane;
-        uint32_t acc[P][4] = {};
-        int z = 0;
-        asm volatile("" : "+s"(z));
-        with_phase(phase_of(t), [&](auto phc) __attribute__((always_inline)) {
-          tile_body(phc, acc, off, [&](auto& feed) __attribute__((always_inline)) {
-            int j = 0;
-            for (; j + U <= k; j += U) {
-              uint4 x[U];
-              load_grp<U>(x, sp, j, off, len);
-              if constexpr (SL == 3)
-                mac_feed_pipe<P, U, X0, decltype(phc)::value>(acc, x, j, tbl + z, la + threadIdx.x, kLa,
-                                                              lt, x0src);
-              else
-                mac_feed<P, U, X0>(acc, x, j, tbl + z, feed, x0src);
-            }
-            for (; j < k; ++j) {
-              uint4 x[1];
-              load_grp<1>(x, sp, j, off, len);
-              mac_feed<P, 1, X0>(acc, x, j, tbl + z, feed, x0src);
-            }
-          });
-        });
-      }
+        for (int l = 0; l < P; ++l) {
+          store16<kNT>(sp[k + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
+          if (!(X0 && l == 0)) ao[l] = chain_step_sl<PH>(lt, ao[l], acc[l][0], acc[l][1], acc[l][2], acc[l][3]);
+        }
+      });
     }
     if (ragged && blk + 1 == nblk) {  // encode the tail tile; combine checksums it
       const long long off = static_cast<long long>(nfull) * kTile + lane;
@@ -914,121 +633,61 @@ __global__ __launch_bounds__(kBlock * NV, (fused64_waves<P, U, REG>())) void ec_
     }
     if constexpr (X0) {  // row 0 = XOR of the sources in x0src: so is its chain
       uint64_t v = 0;
-      if constexpr (REG) {
-#pragma unroll
-        for (int j = 0; j < U; ++j)
-          if ((x0src >> j) & 1ull) v ^= ra[j];
-      } else {
-        for (int j = 0; j < k; ++j)
-          if ((x0src >> j) & 1ull) v ^= la[j * kLa + threadIdx.x];
-      }
+      for (int j = 0; j < k; ++j)
+        if ((x0src >> j) & 1ull) v ^= la[j * kLa + threadIdx.x];
       ao[0] = v;
     }
     uint64_t* pp = part + (static_cast<size_t>(stripe) * nsh * nblk + blk) * kBlock + tid;
     const size_t sstep = static_cast<size_t>(nblk) * kBlock;
-    if constexpr (REG) {
-#pragma unroll
-      for (int j = 0; j < U; ++j) pp[j * sstep] = to_reg(ra[j]);
-    } else {
-      for (int j = 0; j < k; ++j) pp[j * sstep] = to_reg(la[j * kLa + threadIdx.x]);
-    }
+    for (int j = 0; j < k; ++j) pp[j * sstep] = to_reg(la[j * kLa + threadIdx.x]);
 #pragma unroll
     for (int l = 0; l < P; ++l) pp[(k + l) * sstep] = to_reg(ao[l]);
   }
 }
 
-// Sources per load group of the fused kernel: the largest candidate dividing
-// k (ISAL_HIP_CRC64_FUSED_U overrides it, when it divides k, for tuning).
+// Sources per load group of the fused kernel: the largest candidate dividing k.
 int group_u(int k) {
   static const int cand[] = {12, 10, 8, 6, 5, 4};
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_FUSED_U);
-  if (v > 0) {
-    for (int u : cand)
-      if (v == u && k >= u && k % u == 0) return u;
-  }
   for (int u : cand)
     if (k >= u && k % u == 0) return u;
   return 4;
 }
 
-// Paired chain steps in the fused kernel (ISAL_HIP_CRC64_FUSED_PAIR=0: off).
-int pair_step() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_FUSED_PAIR) != 0;
-}
-
-// Source chains in registers when the k sources form one load group only with
-// ISAL_HIP_CRC64_SRC_CHAIN=reg: on the C2 shape the register variant (209
-// VGPRs, 2 waves/SIMD) is 5 % slower than LDS chains at 3 waves/SIMD
-// (profiles/r01/r01_encode_crc64_sweep.txt).
-bool src_chain_reg64() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC64_SRC_CHAIN) == 1;  // "reg"
-}
-
-// Slicing-by-8 chunk path in the fused kernel: on by default
-// (ISAL_HIP_CRC64_SLICE=0 selects the field tables). C2 step, LDS chains, two
-// lane groups: 4.58 -> 4.01 ms (VALU 2.40e9 -> 1.83e9 wave-instructions,
-// profiles/r02/r02_fastcrc_*); with register chains (240 VGPRs) it is slower.
-// 0: field tables, 1: byte (slicing) tables, 2: hybrid tables (experiment,
-// instantiated for the C2 load group U = 10 only; other U use byte tables),
-// 3 (the default; byte tables elsewhere): byte tables with the chain steps
-// pipelined into the GF rows, for load group U = 10 and P <= 4 — C2 step
-// 3.386 -> 3.305 ms (profiles/r03/r03_pipe64_benches.jsonl).
-int slice64() {
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_SLICE);
-  return v == 0 ? 0 : v == 1 ? 1 : v == 2 ? 2 : 3;
-}
-
-// 256-lane groups per workgroup of the LDS-chain fused kernel: the knob
-// (ISAL_HIP_CRC64_FUSED_NV = 1 or 2) or, unset, 2 when that fits more lane
-// groups on a CU (160 KiB of LDS; the static tables are shared by a workgroup,
-// the source chains are per lane).
+// 256-lane groups per workgroup: 2 when that fits more lane groups on a CU
+// (160 KiB of LDS; the tables are shared by a workgroup, the source chains are
+// per lane). The pipelined path holds 140 VGPRs (3 waves per SIMD): a 512-lane
+// workgroup (8 waves) would leave one workgroup, 2 waves per SIMD, per CU.
 int fused_nv(int sl, int k) {
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC64_FUSED_NV);
-  const size_t cap = 160 * 1024, tabs = (sl == 2 ? kHyLds : sl ? kSlLds : kKernTab + kCE + kOp) * 8,
+  const size_t cap = 160 * 1024, tabs = static_cast<size_t>(kSlLds) * 8,
                la = static_cast<size_t>(k) * kBlock * 8;
   if (tabs + 2 * la >= cap) return 1;  // leave LDS headroom: never the whole 160 KiB
-  if (v == 1 || v == 2) return static_cast<int>(v);
-  // the pipelined path holds 140 VGPRs (3 waves/SIMD): a 512-lane workgroup
-  // (8 waves) would leave one workgroup, 2 waves/SIMD, per CU
   if (sl == 3) return 1;
   return 2 * (cap / (tabs + 2 * la)) > cap / (tabs + la) ? 2 : 1;
 }
 
+// The chain steps pipelined into the GF rows (SL 3) for load group U = 10 and
+// P <= 4 — C2 step 3.386 -> 3.305 ms (profiles/r03/r03_pipe64_benches.jsonl);
+// elsewhere after each pair's GF work (SL 1).
 template <int P, int U>
 void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride,
                     const uint32_t* tbl, int len, int k, unsigned nitems,
                     const isal_hip_crc64_geom& g, const isal_hip_xrows& xr, int refl,
                     const uint64_t* tabs, uint64_t* part) {
   const int ragged = g.tail != 0;
-#define FUSED64_LAUNCH(REG, X0, SL, NV)                                                           \
-  hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, REG, X0, SL, NV>), dim3((grid + NV - 1) / NV),     \
-                     dim3(kBlock * NV), REG ? 0 : lds * NV, s, ptrs, ptr_stride, tbl, len, k,      \
-                     nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),          \
-                     static_cast<unsigned>(g.nfull), ragged, pair_step(), xr.src[0], !refl, tabs, part, \
-                     xcd_order())
-#define FUSED64_X0(REG, SL, NV)                                                                    \
-  do {                                                                                             \
-    if (xr.rows & 1u) FUSED64_LAUNCH(REG, true, SL, NV); else FUSED64_LAUNCH(REG, false, SL, NV); \
-  } while (0)
   const size_t lds = static_cast<size_t>(k) * kBlock * 8;
-  const bool reg = k == U && src_chain_reg64();
-  int sl = slice64();
-  if ((sl == 2 || sl == 3) && (U != 10 || reg || P > 4)) sl = 1;
-  const bool nv2 = !reg && fused_nv(sl, k) == 2;
-  if (reg) {
-    if (sl) FUSED64_X0(true, 1, 1); else FUSED64_X0(true, 0, 1);
-  } else if (sl == 2) {
-    if constexpr (U == 10) {
-      if (nv2) FUSED64_X0(false, 2, 2); else FUSED64_X0(false, 2, 1);
-    }
-  } else if (sl == 3) {
-    if constexpr (U == 10 && P <= 4) {
-      if (nv2) FUSED64_X0(false, 3, 2); else FUSED64_X0(false, 3, 1);
-    }
-  } else if (sl) {
-    if (nv2) FUSED64_X0(false, 1, 2); else FUSED64_X0(false, 1, 1);
+#define FUSED64_LAUNCH(X0, SL, NV)                                                                 \
+  hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, X0, SL, NV>), dim3((grid + NV - 1) / NV),           \
+                     dim3(kBlock * NV), lds * NV, s, ptrs, ptr_stride, tbl, len, k, nitems,         \
+                     static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),                    \
+                     static_cast<unsigned>(g.nfull), ragged, xr.src[0], !refl, tabs, part)
+#define FUSED64_X0(SL, NV)                                                                        \
+  do {                                                                                            \
+    if (xr.rows & 1u) FUSED64_LAUNCH(true, SL, NV); else FUSED64_LAUNCH(false, SL, NV);           \
+  } while (0)
+  if constexpr (U == 10 && P <= 4) {
+    FUSED64_X0(3, 1);
   } else {
-    if (nv2) FUSED64_X0(false, 0, 2); else FUSED64_X0(false, 0, 1);
+    if (fused_nv(1, k) == 2) FUSED64_X0(1, 2); else FUSED64_X0(1, 1);
   }
 #undef FUSED64_X0
 #undef FUSED64_LAUNCH
@@ -1114,28 +773,14 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
     uint64_t* part = d_part + static_cast<size_t>(s0) * nsh * g.nblk * kBlock;
     if (g.nblk) {
       const unsigned nitems = static_cast<unsigned>(ns * nsh * g.nblk);
-#define SHARDS_LAUNCH(V, M, B)                                                                \
-  hipLaunchKernelGGL((crc64_shards<V, M, B>), dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, \
-                     len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),      \
-                     static_cast<unsigned>(g.nfull), d_tabs, part)
-      const int m = chain_step(), b8 = load_batch() == 8;
-      if (vec16 && shards_pre()) {
-#define PRE_LAUNCH(B, PP)                                                                               \
-  hipLaunchKernelGGL((crc64_shards_pre<B, PP>), dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, \
-                     len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),          \
-                     static_cast<unsigned>(g.nfull), !refl, d_tabs, part, xcd_order())
-        if (pre_pipe()) { if (b8) PRE_LAUNCH(8, true); else PRE_LAUNCH(4, true); }
-        else { if (b8) PRE_LAUNCH(8, false); else PRE_LAUNCH(4, false); }
-#undef PRE_LAUNCH
-      } else if (!vec16)
-        SHARDS_LAUNCH(false, 1, 4);
-      else if (m == 4)
-        { if (b8) SHARDS_LAUNCH(true, 4, 8); else SHARDS_LAUNCH(true, 4, 4); }
-      else if (m == 2)
-        { if (b8) SHARDS_LAUNCH(true, 2, 8); else SHARDS_LAUNCH(true, 2, 4); }
+      if (vec16)
+        hipLaunchKernelGGL(crc64_shards_pre, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, nitems,
+                           static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
+                           static_cast<unsigned>(g.nfull), !refl, d_tabs, part);
       else
-        { if (b8) SHARDS_LAUNCH(true, 1, 8); else SHARDS_LAUNCH(true, 1, 4); }
-#undef SHARDS_LAUNCH
+        hipLaunchKernelGGL(crc64_shards_bytes, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, nitems,
+                           static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
+                           static_cast<unsigned>(g.nfull), d_tabs, part);
       isal_hip_count_launch();
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return static_cast<int>(e);

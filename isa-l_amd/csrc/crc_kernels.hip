@@ -177,29 +177,16 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t crc_mulmod(uint32_t 
 // one 16-byte load in flight per lane leaves the kernel latency-bound.
 constexpr unsigned kCrcBatch = 8;
 
-// M > 1 advances the chain M tiles per step:
-//   a = Z^(4096*M)(a) ^ XOR_h (Z^(4096*(M-1-h)) o crc(0, .))(chunk_h)
-// with the shifted chunk maps of the EXT tables: 7 + 28*M lookups per M tiles
-// instead of 35*M.
-template <int M>
-constexpr int shards_lds_dw() {
-  return kCrcTabDw + (M > 1 ? (M - 1) * ISAL_HIP_CRC_CHUNK_DWORDS + ISAL_HIP_CRC_FIELDS * 32 : 0);
-}
-
-template <bool VEC, int M>
-__global__ __launch_bounds__(kBlock) void crc32c_shards(
+// Shards that are not 16-byte aligned (byte loads, one Z^4096 chain step per
+// tile); aligned shards take crc32c_shards_pre below. (A chain step of four
+// tiles through the shifted chunk maps measured 2.90 vs 2.87 ms per C2 step,
+// profiles/r01/r01_crc_step_sweep.txt; it and its knob were removed in round 5.)
+__global__ __launch_bounds__(kBlock) void crc32c_shards_bytes(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int idx0, int nsh, int len,
     unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, unsigned ntiles,
     const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part, uint32_t* __restrict__ tail,
     int nshard_total, int shard0) {
-  static_assert(kCrcBatch % M == 0, "chain step divides the load batch");
-  __shared__ uint32_t lt[shards_lds_dw<M>()];
-  if constexpr (M > 1) {
-    // chunk maps m = 1..3, then Z^(4096*4)
-    static_assert(M == 4, "EXT tables hold the step-4 shift only");
-    for (int i = threadIdx.x; i < shards_lds_dw<M>() - kCrcTabDw; i += kBlock)
-      lt[kCrcTabDw + i] = tabs[ISAL_HIP_CRC_EXT_TAB + i];
-  }
+  __shared__ uint32_t lt[kCrcTabDw];
   load_crc_tables(lt, tabs);
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned si = w / nblk, blk = w - si * nblk;
@@ -208,59 +195,18 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards(
     const size_t shard = static_cast<size_t>(stripe) * nshard_total + shard0 + i;
     const unsigned t0 = blk * tt, t1 = t0 + tt < ntiles ? t0 + tt : ntiles;
     uint32_t a = 0;
-    unsigned t = t0;
-    if constexpr (VEC) {
-      const unsigned tf = t1 < nfull ? t1 : nfull;  // full tiles of this block
-      // double-buffered: batch b+1 is in flight while batch b is checksummed
-      uint4 xn[kCrcBatch];
-      const long long lane = threadIdx.x * kVec;
-      if (t + kCrcBatch <= tf) {
-#pragma unroll
-        for (unsigned g = 0; g < kCrcBatch; ++g)
-          xn[g] = load16<kBufNT>(base, static_cast<long long>(t + g) * kTile + lane, len);
-      }
-      for (; t + kCrcBatch <= tf; t += kCrcBatch) {
-        uint4 x[kCrcBatch];
-#pragma unroll
-        for (unsigned g = 0; g < kCrcBatch; ++g) x[g] = xn[g];
-        if (t + 2 * kCrcBatch <= tf) {
-#pragma unroll
-          for (unsigned g = 0; g < kCrcBatch; ++g)
-            xn[g] = load16<kBufNT>(base, static_cast<long long>(t + kCrcBatch + g) * kTile + lane, len);
-        }
-        if constexpr (M == 1) {
-#pragma unroll
-          for (unsigned g = 0; g < kCrcBatch; ++g) a = shift_tile(lt, a) ^ chunk_crc(lt, x[g]);
-        } else {
-#pragma unroll
-          for (unsigned g = 0; g < kCrcBatch; g += M) {
-            uint32_t c = chunk_crc(lt, x[g + M - 1]);
-#pragma unroll
-            for (int h = 0; h < M - 1; ++h)
-              c ^= chunk_map(lt + kCrcTabDw + (M - 2 - h) * ISAL_HIP_CRC_CHUNK_DWORDS, x[g + h].x,
-                             x[g + h].y, x[g + h].z, x[g + h].w);
-            a = lookup7(lt + kCrcTabDw + (M - 1) * ISAL_HIP_CRC_CHUNK_DWORDS, a) ^ c;
-          }
-        }
-      }
-    }
-    for (; t < t1; ++t) {
+    for (unsigned t = t0; t < t1; ++t) {
       const long long off = static_cast<long long>(t) * kTile + threadIdx.x * kVec;
       const long long left = len - off;
       const int nb = left >= kVec ? kVec : (left > 0 ? static_cast<int>(left) : 0);
       uint32_t c = 0;
       if (nb == kVec) {
-        if constexpr (VEC) {
-          c = chunk_crc(lt, load16<kBufNT>(base, off, len));
-        } else {
-          const uint8_t* p = reinterpret_cast<const uint8_t*>(base) + off;
-          uint32_t v[4];
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(base) + off;
+        uint32_t v[4];
 #pragma unroll
-          for (int d = 0; d < 4; ++d)
-            v[d] = p[4 * d] | (p[4 * d + 1] << 8) | (p[4 * d + 2] << 16) |
-                   (static_cast<uint32_t>(p[4 * d + 3]) << 24);
-          c = chunk_crc(lt, v[0], v[1], v[2], v[3]);
-        }
+        for (int d = 0; d < 4; ++d)
+          v[d] = p[4 * d] | (p[4 * d + 1] << 8) | (p[4 * d + 2] << 16) | (static_cast<uint32_t>(p[4 * d + 3]) << 24);
+        c = chunk_crc(lt, v[0], v[1], v[2], v[3]);
       } else if (nb > 0) {
         c = bytes_crc(lt, reinterpret_cast<const uint8_t*>(base) + off, nb);
       }
@@ -285,7 +231,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards_pre(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int idx0, int nsh, int len,
     unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull, unsigned ntiles,
     const uint32_t* __restrict__ tabs, uint32_t* __restrict__ part, uint32_t* __restrict__ tail,
-    int nshard_total, int shard0, int xcd) {
+    int nshard_total, int shard0) {
   __shared__ uint32_t lt[kPreFZ + ISAL_HIP_CRC_CHUNK_DWORDS];
   for (int i = threadIdx.x; i < kPreFZ; i += kBlock) lt[i] = tabs[i];
   for (int i = threadIdx.x; i < ISAL_HIP_CRC_CHUNK_DWORDS; i += kBlock)
@@ -296,8 +242,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards_pre(
     return t + 1 == tf ? chunk_map(lt + kPreF, x.x ^ b, x.y, x.z, x.w)
                        : chunk_map(lt + kPreFZ, x.x ^ b, x.y, x.z, x.w);
   };
-  for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
-    const unsigned w = xcd_item(ww, nitems, xcd);
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned si = w / nblk, blk = w - si * nblk;
     const unsigned stripe = si / nsh, i = si - stripe * nsh;
     const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + idx0 + i];
@@ -380,19 +325,6 @@ __global__ __launch_bounds__(kBlock) void crc32c_combine(
 }
 
 constexpr unsigned kMaxCrcItems = 1u << 30;
-
-// Tiles per chain step of crc32c_shards (ISAL_HIP_CRC_STEP = 1 or 4). Unlike
-// CRC64 the CRC32C kernel is not bound by its lookups: step 4 measured 2.90 ms
-// vs 2.87 ms per C2 step (profiles/r01/r01_crc_step_sweep.txt), so 1 by default.
-// Pre-shifted chains in the checksum-only kernel (ISAL_HIP_CRC_PRE=0: the
-// chain-step kernel, with ISAL_HIP_CRC_STEP).
-bool crc_pre() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC_PRE) != 0;
-}
-
-int crc_step() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC_STEP) == 4 ? 4 : 1;
-}
 
 unsigned crc_grid(unsigned long long nitems) {
   return static_cast<unsigned>(nitems);
@@ -711,33 +643,19 @@ int enc_group_crc(int k) {
   return 4;
 }
 
-// Source chains in registers when the k sources form one load group only with
-// ISAL_HIP_CRC_SRC_CHAIN=reg: the register variant needs 153 VGPRs (3 waves
-// per SIMD) and was 2 % behind LDS chains on the C2 shape already in round 1
-// (profiles/r01/r01_crc_tile_sweep.txt); LDS chains (117 VGPRs, 4 waves) also
-// take the X0 variant.
-bool src_chain_reg() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC_SRC_CHAIN) == 1;  // "reg"
-}
-
-// Dwords per chunk through the byte tables in the fused kernel with LDS
-// source chains: all four by default (ISAL_HIP_CRC_BYTE_DWORDS=0 selects the
-// field tables). C2 step 3.74 -> 3.48 ms (VALU 2.11e9 -> 1.65e9
-// wave-instructions; the LDS array is then ~76 % busy, half of it bank
-// conflicts: profiles/r02/r02_fastcrc_*).
-int crc_byte_dwords() {
-  return isal_hip_knob(ISAL_HIP_KNOB_CRC_BYTE_DWORDS) == 0 ? 0 : 4;
-}
-
-// 256-lane groups per workgroup of the byte-path kernel with LDS source
-// chains: 2 when that fits more groups on a CU (160 KiB of LDS: 32 KiB of
-// tables per workgroup, 1 KiB of chains per source and group), else 1;
-// ISAL_HIP_CRC_FUSED_NV = 1 or 2 forces it where it fits.
+// 256-lane groups per workgroup of the fused kernel: 2 when that fits more
+// groups on a CU (160 KiB of LDS: 32 KiB of byte tables per workgroup, 1 KiB
+// of chains per source and group), else 1.
+//
+// Round 5 removed the variants measured slower and their knobs: source chains
+// in registers (ISAL_HIP_CRC_SRC_CHAIN=reg: 153 VGPRs, 3 waves per SIMD, 2 %
+// behind LDS chains on C2, profiles/r01/r01_crc_tile_sweep.txt) and the 5-bit
+// field tables with a Z^4096 step for the sources (ISAL_HIP_CRC_BYTE_DWORDS=0:
+// C2 step 3.48 -> 3.74 ms, profiles/r02/r02_fastcrc_*); the byte tables stay
+// the fused kernel's chunk path.
 int fused_nv32(int k) {
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_CRC_FUSED_NV);
   const size_t cap = 160 * 1024, tabs = kPosLds * 4, la = static_cast<size_t>(k) * kBlock * 4;
   if (tabs + 2 * la >= cap) return 1;  // leave LDS headroom: never the whole 160 KiB
-  if (v == 1 || v == 2) return static_cast<int>(v);
   return 2 * (cap / (tabs + 2 * la)) > cap / (tabs + la) ? 2 : 1;
 }
 
@@ -752,17 +670,12 @@ void launch_fused(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs
                      src0, dst0, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),               \
                      static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull),                  \
                      static_cast<unsigned>(g.ntiles), xr.src[0], tabs, part, tail, nshard_total,   \
-                     out_shard0, xcd_order())
+                     out_shard0, 0)
   const bool x0 = crc_src && (xr.rows & 1u);
-  const bool nb4 = crc_byte_dwords() == 4;
-  const bool nv2 = nb4 && crc_src && fused_nv32(k) == 2;
+  const bool nv2 = crc_src && fused_nv32(k) == 2;
   if (!crc_src)
     FUSED_LAUNCH(false, false, false, 0, 0, 1);
-  else if (k == U && src_chain_reg())  // one load group: source chains in registers (no X0:
-    FUSED_LAUNCH(true, true, false, 0, 0, 1);  // its 2 extra SGPRs make the register variant spill)
-  else if (!nb4) {
-    if (x0) FUSED_LAUNCH(false, true, true, lds, 0, 1); else FUSED_LAUNCH(false, true, false, lds, 0, 1);
-  } else if (nv2) {
+  else if (nv2) {
     if (x0) FUSED_LAUNCH(false, true, true, lds, 4, 2); else FUSED_LAUNCH(false, true, false, lds, 4, 2);
   } else {
     if (x0) FUSED_LAUNCH(false, true, true, lds, 4, 1); else FUSED_LAUNCH(false, true, false, lds, 4, 1);
@@ -836,24 +749,16 @@ extern "C" int isal_hip_launch_crc(const uint64_t* d_ptrs, int ptr_stride, int i
     const uint64_t* ptrs = d_ptrs + s0 * ptr_stride;
     uint32_t* part = d_part + static_cast<size_t>(s0) * nshard_total * g.nblk * kBlock;
     uint32_t* tail = d_tail + static_cast<size_t>(s0) * nshard_total * kBlock;
-#define CRC_SHARDS(V, M)                                                                    \
-  hipLaunchKernelGGL((crc32c_shards<V, M>), dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,     \
-                     ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),           \
-                     static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),                   \
-                     static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0)
-    if (vec16 && crc_pre())
+    if (vec16)
       hipLaunchKernelGGL(crc32c_shards_pre, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
                          ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
                          static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
-                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0,
-                         xcd_order());
-    else if (!vec16)
-      CRC_SHARDS(false, 1);
-    else if (crc_step() == 4)
-      CRC_SHARDS(true, 4);
+                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
     else
-      CRC_SHARDS(true, 1);
-#undef CRC_SHARDS
+      hipLaunchKernelGGL(crc32c_shards_bytes, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
+                         ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
+                         static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
+                         static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
     isal_hip_count_launch();
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);

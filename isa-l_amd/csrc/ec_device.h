@@ -91,11 +91,11 @@ __device__ __forceinline__ void store16(uint64_t base, long long off, uint4 v, i
   }
 }
 
-// Tuning policy of the vector encode kernel (tools/ec_probe.hip explores others).
+// Tuning policy of the vector encode kernel (isa-l_amd/tools/ec_probe.hip explores others).
 //   U      sources whose loads are issued together before any arithmetic
 //   LD/ST  memory access modes of source loads / parity stores (above)
-//   ORDER  0: work item = (stripe, tile) with tile fastest; 1: stripe fastest;
-//          2: XCD-contiguous
+//   ORDER  work order (EncOrder in ec_kernels.hip): 0 = (stripe, tile) with
+//          tile fastest, 2 = XCD-contiguous (the library's); the probe adds others
 // Measured on MI355X (profiles/r01/r01_probe_variants_*.txt): non-temporal loads
 // AND stores lift the 10-read/4-write stream from 5.5 to 6.1 TB/s, issuing
 // all of a stripe's source loads at once (U = k) adds ~1 %, buffer ops ~1 %;
@@ -123,11 +123,6 @@ __device__ __forceinline__ unsigned xcd_item(unsigned w, unsigned n, int on, uns
   if (!on || n % (8 * nv)) return w;
   const unsigned u = w / nv, g = w - u * nv, per = n / (8 * nv);
   return ((u & 7) * per + (u >> 3)) * nv + g;
-}
-
-// ISAL_HIP_XCD_ORDER: the update and CRC kernels' item order (host side).
-[[maybe_unused]] int xcd_order() {
-  return isal_hip_knob(ISAL_HIP_KNOB_XCD_ORDER) == 1;
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {

@@ -36,13 +36,38 @@
 namespace {
 
 
+// Work order of the vector encode: work item w of nitems -> (stripe, 4 KiB
+// column tile). 0: tile fastest. 2 (the library's): XCD-contiguous — blocks
+// b, b+8, b+16.. (one XCD under round-robin dispatch) walk one contiguous
+// eighth of the items (round 3: -1.0 to -1.3 % per C2 step,
+// profiles/r03/r03_enc_order_benches.jsonl); the identity when nitems % 8 != 0.
+// The probe (isa-l_amd/tools/ec_probe.hip) specialises further orders.
+template <int ORDER>
+struct EncOrder;
+
+template <>
+struct EncOrder<0> {
+  __device__ static void item(unsigned w, unsigned nitems, unsigned tiles, unsigned& stripe, unsigned& tile) {
+    stripe = w / tiles;
+    tile = w - stripe * tiles;
+  }
+};
+
+template <>
+struct EncOrder<2> {
+  __device__ static void item(unsigned w, unsigned nitems, unsigned tiles, unsigned& stripe, unsigned& tile) {
+    const unsigned v = xcd_item(w, nitems, 1);
+    stripe = v / tiles;
+    tile = v - stripe * tiles;
+  }
+};
+
 // The work items of an encode launch: (stripe, 4 KiB column tile) pairs.
 template <int P, class Pol, int FL>
 __device__ __forceinline__ void encode_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
                                              int dst0, const uint32_t* __restrict__ tbl, int len, int k,
                                              unsigned nitems, unsigned tiles, unsigned long long r0m,
                                              unsigned c0m) {
-  const unsigned nstripes = nitems / tiles;
   extern __shared__ uint2 enc_lt[];  // kEncLds: {a0, b0} of every coefficient of the pass
   if constexpr ((FL & kEncLds) != 0) {
     for (int i = threadIdx.x; i < k * P; i += kBlock) enc_lt[i] = make_uint2(tbl[i * kTbl], tbl[i * kTbl + 2]);
@@ -50,29 +75,7 @@ __device__ __forceinline__ void encode_items(const uint64_t* __restrict__ ptrs, 
   }
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     unsigned stripe, tile;
-    if constexpr (Pol::ORDER == 0) {
-      stripe = w / tiles;
-      tile = w - stripe * tiles;
-    } else if constexpr (Pol::ORDER == 2 || Pol::ORDER == 3 || Pol::ORDER == 5) {
-      // XCD-contiguous: blocks b, b+8, b+16.. (one XCD under round-robin
-      // dispatch) walk one contiguous eighth of the items (order 2); orders
-      // 3 and 5 (probes) cut the items into 16 / 32 ranges instead, two / four
-      // per XCD. Speed only.
-      constexpr unsigned G = Pol::ORDER == 2 ? 8 : Pol::ORDER == 3 ? 16 : 32;
-      const unsigned per = nitems / G;
-      const unsigned v = (nitems % G) ? w : (w % G) * per + w / G;
-      stripe = v / tiles;
-      tile = v - stripe * tiles;
-    } else if constexpr (Pol::ORDER == 4) {
-      // probe: XCD x streams whole stripes s = x (mod 8), tile fastest
-      const unsigned j = w >> 3, x = w & 7;
-      const unsigned sj = j / tiles;
-      stripe = (nstripes & 7) ? w / tiles : sj * 8 + x;
-      tile = (nstripes & 7) ? w - (w / tiles) * tiles : j - sj * tiles;
-    } else {
-      tile = w / nstripes;
-      stripe = w - tile * nstripes;
-    }
+    EncOrder<Pol::ORDER>::item(w, nitems, tiles, stripe, tile);
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
@@ -460,9 +463,8 @@ __device__ __forceinline__ void mad_bytes(const uint64_t* __restrict__ sp, int s
 template <int P, int ST = kBufNT>
 __device__ __forceinline__ void update_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src_idx,
                                              int dst0, const uint32_t* __restrict__ tbl, int len,
-                                             unsigned nitems, unsigned tiles, int xcd) {
-  for (unsigned ww = blockIdx.x; ww < nitems; ww += gridDim.x) {
-    const unsigned w = xcd_item(ww, nitems, xcd);
+                                             unsigned nitems, unsigned tiles) {
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned stripe = w / tiles;
     const unsigned tile = w - stripe * tiles;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
@@ -540,8 +542,8 @@ template <int P>
 __global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restrict__ ptrs,
                                                         int ptr_stride, int src_idx, int dst0,
                                                         const uint32_t* __restrict__ tbl, int len,
-                                                        unsigned nitems, unsigned tiles, int xcd) {
-  update_items<P>(ptrs, ptr_stride, src_idx, dst0, tbl, len, nitems, tiles, xcd);
+                                                        unsigned nitems, unsigned tiles) {
+  update_items<P>(ptrs, ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
 }
 
 // One update call whose pointers (source, then P parity rows) and the source's
@@ -550,7 +552,7 @@ template <int P>
 __global__ __launch_bounds__(kBlock) void ec_update_karg(const isal_hip_karg a, const isal_hip_kdone d, int len,
                                                          unsigned tiles) {
   const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
-  update_items<P, kBufSC1NT>(ka->ptrs, 1 + P, 0, 1, ka->tbl, len, tiles, tiles, 0);
+  update_items<P, kBufSC1NT>(ka->ptrs, 1 + P, 0, 1, ka->tbl, len, tiles, tiles);
   karg_done(d, (len & (kVec - 1)) != 0 && blockIdx.x == gridDim.x - 1);
 }
 
@@ -578,11 +580,16 @@ constexpr unsigned kMaxItems = 1u << 30;  // keep w / tiles in 32-bit scalar mat
 // chose it was removed in round 5.)
 unsigned grid_for(unsigned nitems) { return nitems; }
 
-// Ring slots of the LDS-DMA staged wide encode (ec_encode_glds): 0 = off.
+// Passes of 5-8 rows stage their sources through the LDS-DMA ring
+// (ec_encode_glds, 4 slots per wave; ISAL_HIP_ENC_GLDS=0 off). Same box, two
+// interleaved rounds (profiles/r05/r05_glds_ab.jsonl), fraction of 8 TB/s
+// registers -> ring of 4: k20p6 0.676/0.673 -> 0.677/0.678, k20p8
+// 0.596/0.598 -> 0.603/0.603, k10p8 0.731/0.731 -> 0.736/0.738, k10p6
+// 0.765/0.765 -> 0.766/0.769; rings of 6 and 8 (more LDS, fewer
+// workgroups per CU) were flat to 3.5 % slower and are not built.
+constexpr int kGldsRing = 4;
 int enc_glds(int P) {
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_GLDS);
-  if (P < 5) return 0;
-  return v == 4 || v == 6 || v == 8 ? static_cast<int>(v) : 0;
+  return P >= 5 && isal_hip_knob(ISAL_HIP_KNOB_ENC_GLDS) != 0 ? kGldsRing : 0;
 }
 
 template <int P, int R, int FL>
@@ -597,21 +604,15 @@ void launch_glds(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_str
 }
 
 template <int P>
-void launch_glds_r(int R, bool x, unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
-                   int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles,
-                   unsigned long long r0m, unsigned c0m) {
+void launch_glds_r(bool x, unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
+                   const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long r0m,
+                   unsigned c0m) {
   if constexpr (P >= 5) {
-#define EC_GLDS(r)                                                                                             \
-  if (R == r) {                                                                                                \
-    if (x)                                                                                                     \
-      launch_glds<P, r, kEncXor | kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, \
-                                           c0m);                                                               \
-    else                                                                                                       \
-      launch_glds<P, r, kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);   \
-    return;                                                                                                    \
-  }
-    EC_GLDS(4) EC_GLDS(6) EC_GLDS(8)
-#undef EC_GLDS
+    if (x)
+      launch_glds<P, kGldsRing, kEncXor | kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles,
+                                                   r0m, c0m);
+    else
+      launch_glds<P, kGldsRing, kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
   }
 }
 
@@ -640,23 +641,6 @@ int enc_group(int k, int P = 0) {
   for (int u : cand)
     if (k >= u && k % u == 0) return u;
   return 4;
-}
-
-// Work order of the vector encode (ISAL_HIP_ENC_ORDER): 2 (default) =
-// XCD-contiguous (block b, dispatched round-robin to XCD b % 8, takes item
-// (b % 8) * nitems/8 + b / 8, so each XCD walks one contiguous eighth of the
-// stripes; the identity order when nitems % 8 != 0); 0 = (stripe, tile) with
-// tile fastest. Same items, same arithmetic. C2, same box, three runs each:
-// 2.401 -> 2.379 ms and 2.464 -> 2.436 ms on two boxes
-// (profiles/r03/r03_enc_order_benches.jsonl; the memory probe: +1.2 %).
-int enc_order() {
-  return isal_hip_knob(ISAL_HIP_KNOB_ENC_ORDER) == 0 ? 0 : 2;
-}
-
-// Store policy of the vector encode (ISAL_HIP_ENC_STORE=1: sc1 + nt buffer
-// stores, an A/B knob; default nt).
-bool enc_store_sc1() {
-  return isal_hip_knob(ISAL_HIP_KNOB_ENC_STORE) == 1;
 }
 
 // Low table halves from LDS (kEncLds). Same-box A/B, two runs each
@@ -689,10 +673,9 @@ size_t lds_bytes(int k) {
 // k10p1 0.728 -> 0.748, k10p2 0.731 -> 0.757, k4p2 0.780 -> 0.798, C2 flat;
 // wider passes (4-5 waves by their registers) measured flat to 2 % slower
 // with it (k20p6 0.679 -> 0.664), so they allocate only what they use.
-// ISAL_HIP_ENC_LDS_MIN=bytes sets the minimum for every width, 0 = none.
+// (The ISAL_HIP_ENC_LDS_MIN knob that varied it was removed in round 5.)
 size_t enc_lds_alloc(size_t used, int P) {
-  const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_LDS_MIN);
-  const size_t min = v < 0 ? (P <= 4 ? 32768 : 0) : (v <= 65536 ? static_cast<size_t>(v) : 0);
+  const size_t min = P <= 4 ? 32768 : 0;
   return used > min ? used : min;
 }
 
@@ -720,23 +703,14 @@ template <int P, int U>
 void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
                 int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles,
                 bool x, unsigned long long r0m, unsigned c0m) {
-  if (enc_order() == 2 && enc_store_sc1()) {
-    log_launch<P, EncPol<U, kBufNT, kBufSC1NT, 2>, 0>();
-    hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufSC1NT, 2>>), dim3(grid), dim3(kBlock), 0, s,
-                       ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
-  } else if (enc_order() == 2 && enc_lds(P, x, U) && x)
+  if (enc_lds(P, x, U) && x)
     launch_fl<P, U, kEncXor | kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
-  else if (enc_order() == 2 && enc_lds(P, x, U))
+  else if (enc_lds(P, x, U))
     launch_fl<P, U, kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
-  else if (enc_order() == 2 && x)
+  else if (x)
     launch_fl<P, U, kEncXor>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
-  else if (enc_order() == 2)
+  else
     launch_fl<P, U, kEncLUT>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
-  else {
-    log_launch<P, EncNT<U>, 0>();
-    hipLaunchKernelGGL((ec_encode_v16<P, EncNT<U>>), dim3(grid), dim3(kBlock), 0, s, ptrs,
-                       ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
-  }
 }
 
 template <int P>
@@ -747,8 +721,8 @@ hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
   const unsigned nitems = nstripes * tiles;
   const unsigned grid = grid_for(nitems);
-  if (vec16 && enc_glds(P) && enc_order() == 2) {
-    launch_glds_r<P>(enc_glds(P), x, grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+  if (vec16 && enc_glds(P)) {
+    launch_glds_r<P>(x, grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
   } else if (vec16) {
     switch (enc_group(k, P)) {
 #define EC_GROUP(u)                                                                                   \
@@ -773,13 +747,11 @@ hipError_t update_pass(const uint64_t* ptrs, int ptr_stride, int src_idx, int ds
   const unsigned span = vec16 ? kTile : kBlock;
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
   const unsigned nitems = nstripes * tiles;
-  // ISAL_HIP_UPD_LDS_MIN=bytes: dynamic LDS per update workgroup, an occupancy
-  // cap for A/B runs (as enc_lds_alloc; default none)
-  const long long um = isal_hip_knob(ISAL_HIP_KNOB_UPD_LDS_MIN);
-  const size_t ulds = um > 0 && um <= 65536 ? static_cast<size_t>(um) : 0;
+  // (An occupancy cap through dynamic LDS measured flat at 8 workgroups per
+  // CU and 2-9 % slower at 4-6, profiles/r04_update_occupancy_ab.jsonl.)
   if (vec16)
-    hipLaunchKernelGGL(ec_update_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), ulds, s, ptrs,
-                       ptr_stride, src_idx, dst0, tbl, len, nitems, tiles, xcd_order());
+    hipLaunchKernelGGL(ec_update_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
+                       ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
   else
     hipLaunchKernelGGL(ec_update_b1<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);

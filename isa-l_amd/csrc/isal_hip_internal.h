@@ -163,45 +163,27 @@ void isal_hip_count_launch(void);
 enum {
         ISAL_HIP_KNOB_BACKEND,       /* auto(0) | gpu(1) | cpu(2); -2 = unknown word */
         ISAL_HIP_KNOB_CPU_MAX_BYTES, /* auto route: host calls up to this many bytes run on the CPU */
-        ISAL_HIP_KNOB_LOG,           /* 1: log every drop-in call's route to stderr */
+        ISAL_HIP_KNOB_LOG,           /* 1: log every drop-in call's route to stderr, 2: + vector encode kernels */
         ISAL_HIP_KNOB_CPU_SIMD,      /* CPU route width cap: 0 per byte, 1 AVX2, 2 GFNI (tests) */
-        ISAL_HIP_KNOB_STAGE_MB,
-        ISAL_HIP_KNOB_ENC_GLDS,      /* wide encode passes staged through LDS by LDS-DMA: ring slots 4|6|8, 0 off */
-        ISAL_HIP_KNOB_CRC_TILES,
-        ISAL_HIP_KNOB_CRC_STEP,
-        ISAL_HIP_KNOB_CRC_SRC_CHAIN, /* lds(0) | reg(1) */
-        ISAL_HIP_KNOB_CRC64_STEP,
-        ISAL_HIP_KNOB_CRC64_BATCH,
-        ISAL_HIP_KNOB_CRC64_FUSED_U,
-        ISAL_HIP_KNOB_CRC64_FUSED_PAIR,
-        ISAL_HIP_KNOB_CRC64_SRC_CHAIN, /* lds(0) | reg(1) */
-        ISAL_HIP_KNOB_CRC_XROWS,       /* 0: checksum 0/1 parity rows too (no derivation) */
-        ISAL_HIP_KNOB_CRC64_SLICE,     /* fused encode+CRC64 chunk path: fields(0) | slice8(1) */
-        ISAL_HIP_KNOB_CRC64_FUSED_NV,  /* 256-lane groups per fused encode+CRC64 workgroup: 1 | 2 */
-        ISAL_HIP_KNOB_CRC_BYTE_DWORDS, /* fused encode+CRC32C: chunk dwords via byte tables, 0 | 4 */
-        ISAL_HIP_KNOB_CRC_FUSED_NV,    /* 256-lane groups per fused encode+CRC32C workgroup: 1 | 2 */
-        ISAL_HIP_KNOB_CRC_PRE,         /* checksum-only CRC32C/CRC64 kernels: pre-shifted chains (default) | 0 */
-        ISAL_HIP_KNOB_FAULT,           /* fault-injection site of GPU-routed calls (tests) */
-        ISAL_HIP_KNOB_FAULT_CHUNK,     /* ... only in this column chunk of a call (tests; unset: every chunk) */
-        ISAL_HIP_KNOB_CHUNK_KB,        /* column-chunk bytes per shard of large host calls (pipelined) */
-        ISAL_HIP_KNOB_PIPE_CHUNKS,     /* 0: large host calls one chunk at a time (no copy overlap) */
-        ISAL_HIP_KNOB_PINNED_DIRECT,   /* 0: stage page-locked host shards like pageable ones */
+        ISAL_HIP_KNOB_STAGE_MB,      /* HBM staging per host call (MiB) */
+        ISAL_HIP_KNOB_ENC_GLDS,      /* 0: wide encode passes (5-8 rows) load through registers, not the LDS-DMA ring */
+        ISAL_HIP_KNOB_CRC_TILES,     /* 4 KiB tiles per CRC workgroup (tests: block geometry) */
+        ISAL_HIP_KNOB_CRC_XROWS,     /* 0: fused checksums compute 0/1 parity rows too (tests: no derivation) */
+        ISAL_HIP_KNOB_FAULT,         /* fault-injection site of GPU-routed calls (tests) */
+        ISAL_HIP_KNOB_FAULT_CHUNK,   /* ... only in this column chunk of a call (tests; unset: every chunk) */
+        ISAL_HIP_KNOB_CHUNK_KB,      /* column-chunk bytes per shard of large host calls (pipelined) */
+        ISAL_HIP_KNOB_PIPE_CHUNKS,   /* 0: large host calls one chunk at a time (no copy overlap) */
+        ISAL_HIP_KNOB_PINNED_DIRECT, /* 0: stage page-locked host shards like pageable ones */
         ISAL_HIP_KNOB_CPU_MAX_BYTES_PINNED, /* auto route limit when every host shard is page-locked */
-        ISAL_HIP_KNOB_PAR_COPY,        /* 0: one thread issues a staged call's copies (no helper) */
-        ISAL_HIP_KNOB_ENC_ORDER,       /* encode work order: 2 XCD-contiguous (default), 0 tile-fastest */
-        ISAL_HIP_KNOB_XCD_ORDER,       /* update / CRC kernels: 1 XCD-contiguous items */
-        ISAL_HIP_KNOB_ENC_STORE,       /* vector encode stores: 1 sc1 + nt (A/B) | nt */
-        ISAL_HIP_KNOB_CRC64_PRE_PIPE,  /* checksum-only CRC64: 1 pipelined lookups (slower; off) */
-        ISAL_HIP_KNOB_ENC_XOR,         /* 0: the encode computes 0/1 rows and columns with lookups too */
-        ISAL_HIP_KNOB_ENC_LDS,         /* encode low table halves from LDS: 1 always, 0 never (default: 5-6 looked-up rows) */
-        ISAL_HIP_KNOB_KARG,            /* 0: device-resident drop-in encodes upload their arguments */
-        ISAL_HIP_KNOB_MAX_HELPERS,     /* copy-out helper threads per process (default 8) */
-        ISAL_HIP_KNOB_KARG_DONE,       /* 0: kernel-argument calls wait in hipStreamSynchronize (no host mailbox) */
-        ISAL_HIP_KNOB_ENC_GROUP,       /* 12/10/8/6/5/4: encode load group forced (tuning A/B) */
-        ISAL_HIP_KNOB_KARG_NARROW,     /* drop-in kernel-argument encode with 4-byte lanes: 1 on, 0 off */
-        ISAL_HIP_KNOB_ENC_WIDE5,       /* 0: 6-8 row passes keep the largest load group (no groups of 5) */
-        ISAL_HIP_KNOB_ENC_LDS_MIN,     /* minimum dynamic LDS per encode workgroup (default 32 KiB for <= 4 rows) */
-        ISAL_HIP_KNOB_UPD_LDS_MIN,     /* dynamic LDS per update workgroup: occupancy cap (A/B, default none) */
+        ISAL_HIP_KNOB_PAR_COPY,      /* 0: one thread issues a staged call's copies (no helper) */
+        ISAL_HIP_KNOB_ENC_XOR,       /* 0: the encode computes 0/1 rows and columns with lookups too */
+        ISAL_HIP_KNOB_ENC_LDS,       /* encode low table halves from LDS: 1 always, 0 never (default: 5-6 looked-up rows) */
+        ISAL_HIP_KNOB_KARG,          /* 0: device-resident drop-in encodes upload their arguments */
+        ISAL_HIP_KNOB_MAX_HELPERS,   /* copy-out helper threads per process (default 8) */
+        ISAL_HIP_KNOB_KARG_DONE,     /* 0: kernel-argument calls wait in hipStreamSynchronize (no host mailbox) */
+        ISAL_HIP_KNOB_ENC_GROUP,     /* 12/10/8/6/5/4: encode load group forced (tests: every group path) */
+        ISAL_HIP_KNOB_KARG_NARROW,   /* drop-in kernel-argument encode with 4-byte lanes: 1 on, 0 off */
+        ISAL_HIP_KNOB_ENC_WIDE5,     /* 0: 6-8 row passes keep the largest load group (no groups of 5) */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

@@ -37,3 +37,12 @@ def gpu():
 
     assert torch.cuda.is_available(), "gpu tests need an MI355X"
     return torch.device("cuda:0")
+
+
+def pytest_terminal_summary(terminalreporter):
+    """Peak resident memory of the test process (the GPU tier's full-size
+    C2/C3/C4 host arrays are freed after each test; DESIGN §5 records it)."""
+    import resource
+
+    kb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    terminalreporter.write_line(f"peak RSS of the test process: {kb / 1024:.0f} MiB")

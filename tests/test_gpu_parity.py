@@ -328,17 +328,13 @@ def test_batch_encode_update_vs_oracle(engine, oracle, gpu):
     b.close()
 
 
-@pytest.mark.parametrize("store", ["0", "1"])
 @pytest.mark.parametrize("k,rows,n,ns", [(10, 4, 65536 + 48, 37), (10, 4, 1 << 20, 16), (7, 3, 4096 * 3, 5)])
-def test_batch_encode_xcd_order_vs_oracle(engine, oracle, gpu, monkeypatch, store, k, rows, n, ns):
-    """The XCD-contiguous work order (ISAL_HIP_ENC_ORDER=2) covers every
+def test_batch_encode_xcd_order_vs_oracle(engine, oracle, gpu, k, rows, n, ns):
+    """The XCD-contiguous work order (EncOrder<2>, the library's) covers every
     (stripe, tile) exactly once: item counts divisible by 8 and not (the
-    identity order then), ragged tiles, == oracle on every stripe; with nt
-    and with sc1 + nt parity stores (ISAL_HIP_ENC_STORE=1)."""
+    identity order then), ragged tiles, == oracle on every stripe."""
     import torch
 
-    _setenv(monkeypatch, "ISAL_HIP_ENC_ORDER", "2")
-    _setenv(monkeypatch, "ISAL_HIP_ENC_STORE", store)
     a = engine.gf_gen_rs_matrix(k + rows, k)
     tbls = engine.ec_init_tables(k, rows, a[k * k:])
     data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 77)
@@ -366,7 +362,8 @@ def _coef_01(rng, k, rows, kind):
     return c.reshape(-1)
 
 
-@pytest.mark.parametrize("xor,lds", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
+@pytest.mark.parametrize("xor,lds,glds", [("1", "1", "1"), ("0", "1", "1"), ("1", "1", "0"), ("0", "1", "0"),
+                                          ("1", "0", "0"), ("0", "0", "0")])
 @pytest.mark.parametrize("k,rows,n,ns,gen", [
     (10, 4, 65536 + 48, 9, "rs"),       # C2 shape class, pairs of sources
     (10, 6, 65536, 8, "rs"),            # P = 6: no pairs
@@ -381,15 +378,18 @@ def _coef_01(rng, k, rows, kind):
     (10, 4, 65536, 5, "mask"), (20, 6, 16384, 3, "mask"), (10, 8, 8192, 3, "mask"),
     (10, 5, 8192, 3, "rowonly"), (10, 4, 8192, 3, "big"),
 ])
-def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, lds, k, rows, n, ns, gen):
+def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, lds, glds, k, rows, n, ns, gen):
     """Rows and columns of 0/1 coefficients (gf_gen_rs_matrix row 0 and column
-    0, RAID P) take XORs instead of v_perm lookups (ISAL_HIP_ENC_XOR), and the
-    low table halves come from LDS (ISAL_HIP_ENC_LDS), both default on: batch
-    and drop-in encode == oracle with each on and off."""
+    0, RAID P) take XORs instead of v_perm lookups (ISAL_HIP_ENC_XOR), the low
+    table halves come from LDS (ISAL_HIP_ENC_LDS) and passes of 5-8 rows stage
+    their sources through the LDS-DMA ring (ISAL_HIP_ENC_GLDS, which always
+    takes the LDS halves), all default on: batch and drop-in encode == oracle
+    with each on and off."""
     import torch
 
     _setenv(monkeypatch, "ISAL_HIP_ENC_XOR", xor)
     _setenv(monkeypatch, "ISAL_HIP_ENC_LDS", lds)
+    _setenv(monkeypatch, "ISAL_HIP_ENC_GLDS", glds)
     if gen == "rs":
         coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
     else:
@@ -421,12 +421,18 @@ def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, l
     (32, 5, 8192, 8, "big"),            # four groups of 8, no 0/1 structure
     (20, 7, 4096, 2, "mask"),           # masks, a group that does not start at source 0
     (36, 12, 8192, 3, "rs"),            # two passes (8 + 4 rows) of three groups of 12
+    (13, 6, 4096 * 5, 3, "rs"),         # odd k: the LDS-DMA ring's single last source
+    (9, 7, 4096 * 4 + 16, 3, "mask"),   # ring of 4 over k = 9: a partial last round
 ])
-def test_encode_load_groups_vs_oracle(engine, oracle, gpu, k, rows, n, ns, gen):
+@pytest.mark.parametrize("glds", ["1", "0"])
+def test_encode_load_groups_vs_oracle(engine, oracle, gpu, monkeypatch, glds, k, rows, n, ns, gen):
     """Stripes of two or more load groups (enc_group: k a multiple of 8, 10 or
     12 above it): batch encode == oracle with ragged tails, odd group counts
-    and two passes."""
+    and two passes; passes of 5-8 rows through the LDS-DMA ring (default) and
+    through registers (ISAL_HIP_ENC_GLDS=0)."""
     import torch
+
+    _setenv(monkeypatch, "ISAL_HIP_ENC_GLDS", glds)
 
     if gen == "rs":
         coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
@@ -487,40 +493,6 @@ def test_dropin_kernel_args_vs_oracle(engine, oracle, gpu, monkeypatch, capfd, n
         assert np.array_equal(out[base + n: base + stride], canary[l * stride + n: (l + 1) * stride]), l
 
 
-def test_xcd_item_order_update_and_checksums(engine, oracle, gpu, monkeypatch):
-    """ISAL_HIP_XCD_ORDER=1 (update, checksum-only and fused CRC kernels take
-    their items XCD-contiguously): item counts that are multiples of 8 (the
-    remapped order) and not (the identity), one and two lane groups, == oracle."""
-    import torch
-
-    _setenv(monkeypatch, "ISAL_HIP_XCD_ORDER", "1")
-    # update: 16 stripes x 17 tiles (a multiple of 8 items) and 37 x 16 + 48 bytes
-    for k, rows, n, ns in [(10, 4, 4096 * 17, 16), (10, 4, 65536 + 48, 37)]:
-        a = engine.gf_gen_rs_matrix(k + rows, k)
-        tbls = engine.ec_init_tables(k, rows, a[k * k:])
-        data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 91)
-        b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
-        for v in range(k):
-            b.update(v, 0)
-        torch.cuda.synchronize()
-        h_data, h_cod = _host(data), _host(coding)
-        want = _oracle_encode_all(oracle, a[k * k:], k, rows, [[h_data[s, j] for j in range(k)] for s in range(ns)])
-        for s in range(ns):
-            for l in range(rows):
-                assert np.array_equal(h_cod[s, l], want[s][l]), (k, n, s, l)
-        b.close()
-    for nv in ("1", "2"):
-        _setenv(monkeypatch, "ISAL_HIP_CRC_FUSED_NV", nv)
-        _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_NV", nv)
-        test_encode_crc_vs_oracle(engine, oracle, gpu, 10, 4, 4096 * 64 * 2, 8, 0)
-        test_encode_crc_vs_oracle(engine, oracle, gpu, 10, 4, 4096 * 37 + 2048, 5, 0)
-        test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 10, 4, 4096 * 64 * 2, 8, 0, None, 1)
-        test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 10, 4, 4096 * 37 + 2048, 3, 0, 4, 5)
-    for variant in (0, 5):
-        test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, 10, 4, 4096 * 64 * 2, 8, 0, None)
-        test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, 5, 2, 4096 * 40, 2, 0, 16)
-
-
 def test_config_c1_cauchy_k4_p2_64k(engine, gpu):
     case = golden()["encode"][0]
     assert (case["k"], case["rows"], case["len"], case["gen"]) == (4, 2, 65536, "cauchy")
@@ -549,6 +521,22 @@ def _oracle_encode_all(oracle, coef, k, rows, srcs, threads=16):
         return list(ex.map(one, srcs))
 
 
+def _check_stripes_vs_oracle(oracle, coef, k, rows, srcs_of, out, ns, chunk=64):
+    """out[s] (device, rows x n) == the oracle's encode of srcs_of(s) (a list
+    of k device shards) for every stripe s, `chunk` stripes at a time so the
+    host holds ~chunk x (k + rows) shards, not the whole batch (the full-size
+    C2/C3 tests used to keep ~20 GiB of host arrays alive)."""
+    for s0 in range(0, ns, chunk):
+        s1 = min(ns, s0 + chunk)
+        srcs = [[_host(x) for x in srcs_of(s)] for s in range(s0, s1)]
+        want = _oracle_encode_all(oracle, coef, k, rows, srcs)
+        got = _host(out[s0:s1])
+        for i in range(s1 - s0):
+            for l in range(rows):
+                assert np.array_equal(got[i, l], want[i][l]), (s0 + i, l)
+        del srcs, want, got
+
+
 def test_config_c2_c3_full_size(engine, oracle, gpu):
     """C2: k=10 p=4, 1 MiB shards x 1024 stripes in one launch; C3: recover 3
     erased data shards {4,6,7} of every stripe. Full size and byte for byte:
@@ -562,12 +550,7 @@ def test_config_c2_c3_full_size(engine, oracle, gpu):
     enc = engine.Batch(n, k, p, engine.ec_init_tables(k, p, a[k * k:]), ns, dptr, cptr)
     enc.encode(0)
     torch.cuda.synchronize()
-    h_data, h_cod = _host(data), _host(coding)
-    want = _oracle_encode_all(oracle, a[k * k:], k, p, [[h_data[s, j] for j in range(k)] for s in range(ns)])
-    for s in range(ns):
-        for l in range(p):
-            assert np.array_equal(h_cod[s, l], want[s][l]), (s, l)
-    del want
+    _check_stripes_vs_oracle(oracle, a[k * k:], k, p, lambda s: [data[s, j] for j in range(k)], coding, ns)
     errs = [4, 6, 7]
     ret, c, surv = ecutil.decode_matrix(a, k, errs)
     assert ret == 0
@@ -578,13 +561,9 @@ def test_config_c2_c3_full_size(engine, oracle, gpu):
     dec = engine.Batch(n, k, len(errs), engine.ec_init_tables(k, len(errs), c), ns, sptr, rptr)
     dec.encode(0)
     torch.cuda.synchronize()
-    h_rec = _host(rec)
-    hfrag = lambda s, i: h_data[s, i] if i < k else h_cod[s, i - k]  # noqa: E731
-    want = _oracle_encode_all(oracle, c, k, len(errs), [[hfrag(s, i) for i in surv] for s in range(ns)])
-    for s in range(ns):
-        for i, e in enumerate(errs):
-            assert np.array_equal(h_rec[s, i], want[s][i]), (s, e)
-            assert np.array_equal(h_rec[s, i], h_data[s, e]), (s, e)
+    _check_stripes_vs_oracle(oracle, c, k, len(errs), lambda s: [frag(s, i) for i in surv], rec, ns)
+    # and the recovered shards are the erased data, every byte (on the device)
+    assert bool(torch.equal(rec, data[:, errs]))
     enc.close()
     dec.close()
 
@@ -1033,34 +1012,6 @@ CRC_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("step", [1, 4])
-@pytest.mark.parametrize("k,rows,n,ns,tt", [(10, 4, 65536, 3, None), (3, 2, 4096 * 45 + 48, 2, 13),
-                                            (2, 1, 4096 * 8, 2, 8), (1, 1, 4096 * 7 + 5, 2, None)])
-def test_crc_chain_step(engine, oracle, gpu, monkeypatch, step, k, rows, n, ns, tt):
-    """crc32c_shards advancing its chain 1 or 4 tiles per step (shifted chunk
-    maps, ISAL_HIP_CRC_STEP) == oracle crc32_iscsi, incl. blocks whose tile
-    count is not a multiple of the load batch."""
-    import torch
-
-    _setenv(monkeypatch, "ISAL_HIP_CRC_PRE", "0")  # the chain-step kernel (pre-shifted is the default)
-    _setenv(monkeypatch, "ISAL_HIP_CRC_STEP", str(step))
-    if tt:
-        _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
-    a = oracle.gf_gen_rs_matrix(k + rows, k)
-    tbls = engine.ec_init_tables(k, rows, a[k * k:].copy())
-    bufs = [fill_bytes(n, 17 * s + j + step) for s in range(ns) for j in range(k + rows)]
-    store = [_dev(torch, h, gpu) for h in bufs]
-    ptr = [int(t.data_ptr()) for t in store]
-    dptr = [ptr[s * (k + rows) + j] for s in range(ns) for j in range(k)]
-    cptr = [ptr[s * (k + rows) + k + l] for s in range(ns) for l in range(rows)]
-    out = torch.zeros(ns * (k + rows), dtype=torch.int32, device=gpu)
-    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
-    b.crc(0x1234567, out, 0)
-    torch.cuda.synchronize()
-    assert [int(v) & 0xFFFFFFFF for v in out.tolist()] == [oracle.crc32_iscsi(h, 0x1234567) for h in bufs]
-    b.close()
-
-
 @pytest.mark.parametrize("k,rows,n,ns,skew", CRC_SHAPES)
 def test_encode_crc_vs_oracle(engine, oracle, gpu, k, rows, n, ns, skew):
     """Fused encode + CRC: parity == oracle encode, every shard's CRC == oracle
@@ -1141,20 +1092,19 @@ def test_encode_crc_tiles_per_workgroup(engine, oracle, gpu, monkeypatch, k, row
     b.close()
 
 
-@pytest.mark.parametrize("chain", ["lds", "reg"])
 @pytest.mark.parametrize("xrows", ["1", "0"])
-@pytest.mark.parametrize("k,n,tt", [(10, 4096 * 37 + 2048, 4), (7, 65536, None), (10, 65536, None)])
-def test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, chain, xrows, k, n, tt):
+@pytest.mark.parametrize("k,n,tt", [(10, 4096 * 37 + 2048, 4), (7, 65536, None), (10, 65536, None),
+                                    (8, 4096 * 21, 2)])
+def test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, xrows, k, n, tt):
     """A parity row 0 whose coefficients are all 0/1 gets its CRC32C / CRC64
     chains from the sources' chains instead of being checksummed
     (ISAL_HIP_CRC_XROWS=1, default; other 0/1 rows, an all-zero row and a
     general row are checksummed); both ways every CRC == the oracle, full and
-    ragged tiles, register and LDS source chains."""
+    ragged tiles; k = 8 takes the CRC64 byte-table path after each pair (two
+    lane groups per workgroup), k = 10 the path pipelined into the rows."""
     import torch
 
     _setenv(monkeypatch, "ISAL_HIP_CRC_XROWS", xrows)
-    _setenv(monkeypatch, "ISAL_HIP_CRC_SRC_CHAIN", chain)    # CRC32C source chains
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_SRC_CHAIN", chain)  # CRC64 source chains
     if tt:
         _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
     rows, ns = 5, 3
@@ -1187,33 +1137,6 @@ def test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, chain, xro
             assert g32[s * (k + rows) + i] == oracle.crc32_iscsi(buf, 0x1234567), (s, i, "crc32c")
             assert g64[s * (k + rows) + i] == oracle.crc64(6, buf, 0xABCDEF), (s, i, "crc64")
     b.close()
-
-
-@pytest.mark.parametrize("nb", ["4", "0"])
-@pytest.mark.parametrize("k,rows,n,ns,skew", CRC_SHAPES)
-def test_encode_crc_byte_tables(engine, oracle, gpu, monkeypatch, nb, k, rows, n, ns, skew):
-    """The fused CRC32C kernel with every chunk dword through the byte-position
-    tables (ISAL_HIP_CRC_BYTE_DWORDS=4, the default) and through the 5-bit
-    field tables (=0) == oracle."""
-    _setenv(monkeypatch, "ISAL_HIP_CRC_BYTE_DWORDS", nb)
-    test_encode_crc_vs_oracle(engine, oracle, gpu, k, rows, n, ns, skew)
-
-
-@pytest.mark.parametrize("tt", [1, 3, 16])
-def test_encode_crc_field_tables_tiles(engine, oracle, gpu, monkeypatch, tt):
-    _setenv(monkeypatch, "ISAL_HIP_CRC_BYTE_DWORDS", "0")
-    test_encode_crc_tiles_per_workgroup(engine, oracle, gpu, monkeypatch, 7, 3, tt)
-
-
-@pytest.mark.parametrize("xrows", ["1", "0"])
-@pytest.mark.parametrize("k,n,tt", [(10, 4096 * 37 + 2048, 4), (7, 65536, None)])
-def test_fused_crc_derived_xor_rows_fast_paths(engine, oracle, gpu, monkeypatch, xrows, k, n, tt):
-    """Derived XOR rows with the byte-table CRC32C path and the slicing CRC64
-    path (two lane groups per workgroup)."""
-    _setenv(monkeypatch, "ISAL_HIP_CRC_BYTE_DWORDS", "4")
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", "1")
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_NV", "2")
-    test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, "lds", xrows, k, n, tt)
 
 
 def test_encode_crc_c2_full_size(engine, oracle, gpu):
@@ -1279,65 +1202,6 @@ def test_crc64_c2_full_size(engine, oracle, gpu):
     b.close()
 
 
-@pytest.mark.parametrize("variant", [0, 5])
-@pytest.mark.parametrize("k,rows,n,ns,skew,tt", [CRC64_SHAPES[0], CRC64_SHAPES[1], CRC64_SHAPES[6],
-                                                 (3, 1, 4096 * 11 + 16, 2, 0, 7), (2, 1, 4096 * 19, 2, 0, 17)])
-def test_crc64_pre_batch8(engine, oracle, gpu, monkeypatch, variant, k, rows, n, ns, skew, tt):
-    """The pre-shifted checksum-only CRC64 kernel with 8 tiles per load batch
-    (ISAL_HIP_CRC64_BATCH=8: crc64_shards_pre<8>), incl. blocks shorter than a
-    batch and not a multiple of it, == oracle."""
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_BATCH", "8")
-    test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, k, rows, n, ns, skew, tt)
-
-
-@pytest.mark.parametrize("batch", [4, 8])
-@pytest.mark.parametrize("variant", [0, 5])
-@pytest.mark.parametrize("k,rows,n,ns,skew,tt", [CRC64_SHAPES[0], CRC64_SHAPES[1], CRC64_SHAPES[6],
-                                                 (3, 1, 4096 * 11 + 16, 2, 0, 7), (2, 1, 4096 * 4, 2, 0, 4),
-                                                 (2, 1, 4096 * 9, 1, 0, 9)])
-def test_crc64_pre_unpipelined(engine, oracle, gpu, monkeypatch, variant, batch, k, rows, n, ns, skew, tt):
-    """The pre-shifted checksum-only CRC64 kernel with and without the
-    pipelined lookups (ISAL_HIP_CRC64_PRE_PIPE=1 / 0: crc64_shards_pre<B,
-    true / false>) == oracle, 4 or 8 tiles per load batch, incl. blocks of
-    exactly one batch (its last tile in the batch) and a batch plus a tail."""
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_PRE_PIPE", "0")
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_BATCH", str(batch))
-    test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, k, rows, n, ns, skew, tt)
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_PRE_PIPE", "1")
-    test_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, variant, k, rows, n, ns, skew, tt)
-
-
-@pytest.mark.parametrize("batch", [4, 8])
-@pytest.mark.parametrize("step", [1, 2, 4])
-@pytest.mark.parametrize("k,rows,n,ns,skew,tt", [CRC64_SHAPES[0], CRC64_SHAPES[1], CRC64_SHAPES[6],
-                                                 (3, 1, 4096 * 11 + 16, 2, 0, 7)])
-def test_crc64_chain_step(engine, oracle, gpu, monkeypatch, step, batch, k, rows, n, ns, skew, tt):
-    """crc64_shards advancing its chain 1, 2 or 4 tiles per step (shifted chunk
-    maps, ISAL_HIP_CRC64_STEP), 4 or 8 tile loads in flight, == oracle, incl. blocks whose tile count is not
-    a multiple of the step."""
-    import torch
-
-    _setenv(monkeypatch, "ISAL_HIP_CRC_PRE", "0")  # the chain-step kernel (pre-shifted is the default)
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_STEP", str(step))
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_BATCH", str(batch))
-    if tt:
-        _setenv(monkeypatch, "ISAL_HIP_CRC_TILES", str(tt))
-    a = oracle.gf_gen_rs_matrix(k + rows, k)
-    tbls = engine.ec_init_tables(k, rows, a[k * k:].copy())
-    bufs = [fill_bytes(n, 31 * s + j + step) for s in range(ns) for j in range(k + rows)]
-    store = [_dev(torch, h, gpu) for h in bufs]
-    ptr = [int(t.data_ptr()) for t in store]
-    dptr = [ptr[s * (k + rows) + j] for s in range(ns) for j in range(k)]
-    cptr = [ptr[s * (k + rows) + k + l] for s in range(ns) for l in range(rows)]
-    out = torch.zeros(ns * (k + rows), dtype=torch.int64, device=gpu)
-    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
-    for variant in (0, 3):
-        b.crc64(variant, 0x5A5A, out, 0)
-        torch.cuda.synchronize()
-        assert _crc64_words(out) == [oracle.crc64(variant, h, 0x5A5A) for h in bufs], variant
-    b.close()
-
-
 ENCODE_CRC64_SHAPES = [
     # k, rows, len, nstripes, byte offset of every shard, tiles/workgroup, variant
     (10, 4, 65536, 5, 0, None, 0),        # C2 shape: source chains in registers
@@ -1394,63 +1258,26 @@ def test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns
     b.close()
 
 
-@pytest.mark.parametrize("pair,chain", [(0, "lds"), (1, "reg"), (0, "reg")])
-@pytest.mark.parametrize("k,rows,n,ns,skew,tt,variant", ENCODE_CRC64_SHAPES[:5])
-def test_encode_crc64_knobs(engine, oracle, gpu, monkeypatch, pair, chain, k, rows, n, ns, skew, tt,
-                            variant):
-    """The fused encode + CRC64 kernel with unpaired chain steps
-    (ISAL_HIP_CRC64_FUSED_PAIR=0) and with register source chains
-    (ISAL_HIP_CRC64_SRC_CHAIN=reg) == oracle as the defaults are."""
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_PAIR", str(pair))
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_SRC_CHAIN", chain)
-    test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant)
-
-
-@pytest.mark.parametrize("slice_,pair,chain,nv", [
-    ("1", 1, "lds", 1), ("1", 0, "lds", 1), ("1", 1, "reg", 1), ("1", 0, "reg", 1),
-    ("1", 1, "lds", 2), ("1", 0, "lds", 2), ("0", 1, "lds", 2), ("0", 0, "lds", 2),
-    ("0", 1, "lds", 1), ("0", 1, "reg", 1), ("2", 1, "lds", 1), ("2", 1, "lds", 2), ("2", 0, "lds", 2),
-    ("3", 1, "lds", 1), ("3", 1, "lds", 2), ("3", 0, "lds", 2)])
-@pytest.mark.parametrize("k,rows,n,ns,skew,tt,variant", ENCODE_CRC64_SHAPES[:5])
-def test_encode_crc64_slice_knobs(engine, oracle, gpu, monkeypatch, slice_, pair, chain, nv, k, rows, n,
-                                  ns, skew, tt, variant):
-    """The slicing-by-8 chunk path of the fused kernel (ISAL_HIP_CRC64_SLICE=1,
-    u-domain chains) and two 256-lane groups per workgroup
-    (ISAL_HIP_CRC64_FUSED_NV=2) == oracle, paired and unpaired steps, both
-    chain homes."""
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", slice_)
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_NV", str(nv))
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_PAIR", str(pair))
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_SRC_CHAIN", chain)
-    test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, ns, skew, tt, variant)
-
-
-@pytest.mark.parametrize("slice_", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("variant", range(8))
-def test_encode_crc64_every_flavour(engine, oracle, gpu, monkeypatch, variant, slice_):
-    """All eight crc64.h flavours through the fused kernel, field-table,
-    slicing, hybrid and pipelined-slicing paths (the u-domain paths byte-swap
-    the norm flavours' chains; the hybrid and pipelined paths exist for load
-    group 10, i.e. the k = 10 case)."""
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", slice_)
+def test_encode_crc64_every_flavour(engine, oracle, gpu, monkeypatch, variant):
+    """All eight crc64.h flavours through the fused kernel's two chunk paths
+    (the u-domain byte-swaps the norm flavours' chains): pipelined into the
+    rows for load group 10 (k = 10), after each pair elsewhere (k = 7)."""
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 10, 4, 4096 * 37 + 2048, 3, 0, 4,
                                 variant)
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, 7, 3, 4096 * 20, 2, 0, 3, variant)
 
 
 @pytest.mark.parametrize("xrows", ["1", "0"])
-@pytest.mark.parametrize("nv", ["1", "2"])
 @pytest.mark.parametrize("k,rows,n,tt,variant", [
     (10, 1, 4096 * 9, None, 0), (10, 2, 4096 * 11 + 1024, 3, 1), (10, 3, 4096 * 8, 2, 2),
     (10, 4, 4096 * 37 + 2048, 4, 5), (20, 3, 4096 * 6 + 512, None, 7), (20, 4, 4096 * 5, 1, 3)])
-def test_encode_crc64_pipelined_rows(engine, oracle, gpu, monkeypatch, xrows, nv, k, rows, n, tt, variant):
-    """ISAL_HIP_CRC64_SLICE=3 (chain steps pipelined into the GF rows): every
-    row count it serves (1..4, rows split over its three stages, one or none
-    of them empty), one and two load groups of 10, row 0 derived or computed,
-    one and two lane groups == oracle."""
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_SLICE", "3")
+def test_encode_crc64_pipelined_rows(engine, oracle, gpu, monkeypatch, xrows, k, rows, n, tt, variant):
+    """The chain steps pipelined into the GF rows (load group 10, 1-4 rows):
+    every row count it serves (rows split over its three stages, one or none
+    of them empty), one and two load groups of 10, row 0 derived or computed
+    == oracle."""
     _setenv(monkeypatch, "ISAL_HIP_CRC_XROWS", xrows)
-    _setenv(monkeypatch, "ISAL_HIP_CRC64_FUSED_NV", nv)
     test_encode_crc64_vs_oracle(engine, oracle, gpu, monkeypatch, k, rows, n, 3, 0, tt, variant)
 
 
@@ -1930,13 +1757,13 @@ def test_bench_rccl_control_plane_single_rank(gpu):
 
 @pytest.mark.parametrize("args,env", [
     (["--k", "10", "--p", "4"], {}),                                  # C2 shape: XOR path, groups of 10
-    (["--k", "10", "--p", "8"], {}),                                  # 8 rows: groups of 5 + LDS halves
+    (["--k", "10", "--p", "8"], {}),                                  # 8 rows: the LDS-DMA ring
     (["--k", "20", "--p", "6", "--len", "262144", "--stripes", "8"], {}),
-    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_WIDE5": "0"}),
-    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_LDS": "0", "ISAL_HIP_ENC_XOR": "0"}),
-    (["--k", "12", "--p", "5"], {"ISAL_HIP_ENC_GROUP": "4"}),
-    (["--k", "10", "--p", "4"], {"ISAL_HIP_ENC_ORDER": "0"}),
-    (["--k", "10", "--p", "4"], {"ISAL_HIP_ENC_STORE": "1"}),
+    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_WIDE5": "0", "ISAL_HIP_ENC_GLDS": "0"}),
+    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_LDS": "0", "ISAL_HIP_ENC_XOR": "0", "ISAL_HIP_ENC_GLDS": "0"}),
+    (["--k", "12", "--p", "5"], {"ISAL_HIP_ENC_GROUP": "4", "ISAL_HIP_ENC_GLDS": "0"}),
+    (["--k", "10", "--p", "8"], {"ISAL_HIP_ENC_GLDS": "0"}),         # 8 rows through registers
+    (["--k", "7", "--p", "5"], {"ISAL_HIP_ENC_XOR": "0"}),            # LDS-DMA ring, lookups only
     (["--workload", "decode"], {}),
 ])
 def test_bench_kernel_label_matches_launch(gpu, args, env):

@@ -50,7 +50,8 @@ HARNESS = {
 def host_info() -> dict:
     """CPU model and core counts of this host (lscpu), plus this process's affinity."""
     info = {"affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
-            "affinity_physical_cores": len(_physical_cpus(0)), "cgroup_cpu_quota": cgroup_cpu_quota()}
+            "affinity_physical_cores": len(_physical_cpus(0)), "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "usable_cores": usable_cores()}
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
         kv = {}
@@ -103,6 +104,18 @@ def physical_cpus(n: int = 0) -> list[int]:
     return _physical_cpus(n)
 
 
+def usable_cores() -> int:
+    """Physical cores this process may use at once: one per physical core of
+    its affinity set, capped by its cgroup CPU quota. (The GPU box grants 16
+    CPUs of quota on a 2 x 64-core host: 128 pinned processes there measured
+    the reference harness at 7.02 GiB/s — what 16 cores give — and the GFNI
+    port at 68 GiB/s against 384 with 16 threads, every thread throttled in
+    turn; profiles/r05/r05_bench_c2_allcores_quota16.json.)"""
+    n = len(_physical_cpus(0))
+    q = cgroup_cpu_quota()
+    return max(1, min(n, int(q))) if q else n
+
+
 def _physical_cpus(n: int) -> list[int]:
     """n (0 = all) CPUs of this process's affinity set, one per physical core where the
     topology says which logical CPUs are hyperthread siblings."""
@@ -124,14 +137,14 @@ def _physical_cpus(n: int) -> list[int]:
 
 
 def run(which: str, procs: int, timeout: float = 180.0) -> dict:
-    """Run `procs` (0 = one per physical core of this process's affinity set)
+    """Run `procs` (0 = usable_cores(): one per physical core this process may use)
     pinned copies of the harness at once (plus nothing else) and sum their
     per-phase MB/s. Returns {phase: {"mb_s_sum", "mb_s_per_proc"}, ...}."""
     argv, names = HARNESS[which]
     exe = os.path.join(REF, argv[0])
     if not os.path.exists(exe):
         return {"error": f"{exe} not built (make -C oracle ref needs /root/reference)"}
-    cpus = _physical_cpus(procs)
+    cpus = _physical_cpus(procs or usable_cores())
 
     def pin(c):
         return lambda: os.sched_setaffinity(0, {c})
@@ -162,7 +175,8 @@ def run(which: str, procs: int, timeout: float = 180.0) -> dict:
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=-1,
-                    help="-1 = 1 and one per physical core of the affinity set; 0 = the latter only")
+                    help="-1 = 1 and usable_cores() (one per physical core of the affinity set, capped "
+                         "by the cgroup CPU quota); 0 = the latter only")
     ap.add_argument("--which", choices=sorted(HARNESS), default="encode")
     a = ap.parse_args(argv)
     out = {"host": host_info()}

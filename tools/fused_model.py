@@ -21,7 +21,8 @@ The kernel cannot run faster than max(valu, lds, hbm); `overlap` is that
 bound over the measured time. A formulation is worth building when the bound
 it implies (fewer VALU, conflict-free LDS) is below the target.
 
-  python3 tools/fused_model.py profiles/r05_pmc_sq_fused.txt > profiles/r05_fused_model.txt
+  python3 tools/fused_model.py profiles/r05/r05_pmc_sq_fused.txt --steady SUB=CSV ... \
+      --compose LABEL=SUB*W+SUB*W > profiles/r05/r05_fused_model.txt
 """
 import json
 import os
@@ -71,35 +72,64 @@ def steady_ms(path, kernel):
     return float(kv["avg_ns"]) / 1e6, int(kv["bytes_per_launch"])
 
 
+def find(counters, sub):
+    hits = [k for k in counters if sub in k]
+    if len(hits) != 1:
+        raise SystemExit(f"fused_model: {sub!r} matches {hits}")
+    return hits[0]
+
+
+def row(label, c, meas_ms, nbytes, rate):
+    valu_ms = c.get("SQ_INSTS_VALU", 0) / CUS / rate / 1e6
+    act = c.get("SQ_LDS_IDX_ACTIVE", 0)
+    conf = c.get("SQ_LDS_BANK_CONFLICT", 0)
+    lds_ms = act / CUS / CLOCK_GHZ / 1e6
+    lds_cf_ms = (act - conf) / CUS / CLOCK_GHZ / 1e6
+    hbm_ms = nbytes / COPY_CEILING * 1e3
+    bound = max(valu_ms, lds_ms, hbm_ms)
+    bound_cf = max(valu_ms, lds_cf_ms, hbm_ms)
+    ov = f"{bound / meas_ms:.3f}" if meas_ms == meas_ms else ""
+    meas = f"{meas_ms:.4f}" if meas_ms == meas_ms else ""
+    print(f"{label},{valu_ms:.3f},{lds_ms:.3f},{lds_cf_ms:.3f},{hbm_ms:.3f},{bound:.3f},{bound_cf:.3f},"
+          f"{meas},{ov},{conf / act if act else 0:.3f}")
+
+
 def main(argv):
-    if len(argv) < 2:
-        print(__doc__)
-        return 2
+    """argv: COUNTERS.txt [--steady SUB=CSV ...] [--compose LABEL=SUB*W+SUB*W ...]"""
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("counters")
+    ap.add_argument("--steady", action="append", default=[], help="kernel substring=steady-state csv")
+    ap.add_argument("--compose", action="append", default=[],
+                    help="LABEL=SUB*W+SUB*W: a formulation not built yet, its counters as a weighted sum "
+                         "of measured kernels' (e.g. the GF half of the encode plus 13/14 of a checksum pass)")
+    ap.add_argument("--bytes", type=float, default=15032385536.0, help="algorithmic bytes per launch")
+    a = ap.parse_args(argv[1:])
     rate = rates()  # wave-instructions per CU per ns
-    counters = sections(argv[1])
-    steady = {}
-    for spec in argv[2:]:  # kernel=steady.csv
-        k, f = spec.split("=", 1)
-        steady[k] = f
-    print(f"# fused-kernel resource model, tools/fused_model.py {' '.join(os.path.relpath(a, ROOT) for a in argv[1:])}")
-    print(f"# VALU issue rate {rate:.3f} wave-instr/CU/ns (r03_valu_probe, 4 waves/SIMD); "
-          f"{CUS} CUs at {CLOCK_GHZ} GHz; HBM at the copy ceiling {COPY_CEILING / 1e12:.2f} TB/s")
+    counters = sections(a.counters)
+    print(f"# fused-kernel resource model: tools/fused_model.py {' '.join(argv[1:])}")
+    print(f"# VALU issue rate {rate:.3f} wave-instr/CU/ns (profiles/r03/r03_valu_probe.jsonl, 4 waves/SIMD); "
+          f"{CUS} CUs at {CLOCK_GHZ} GHz; HBM at the copy ceiling {COPY_CEILING / 1e12:.2f} TB/s; "
+          f"{a.bytes / 1e9:.3f} GB per launch")
     print("kernel,valu_ms,lds_ms,lds_conflict_free_ms,hbm_ms,bound_ms,bound_conflict_free_ms,measured_ms,"
-          "overlap,conflict_share")
-    for kern, c in counters.items():
-        valu_ms = c.get("SQ_INSTS_VALU", 0) / CUS / rate / 1e6
-        act = c.get("SQ_LDS_IDX_ACTIVE", 0)
-        conf = c.get("SQ_LDS_BANK_CONFLICT", 0)
-        lds_ms = act / CUS / CLOCK_GHZ / 1e6
-        lds_cf_ms = (act - conf) / CUS / CLOCK_GHZ / 1e6
-        meas, nbytes = steady_ms(steady[kern], kern) if kern in steady else (float("nan"), 15032385536)
-        hbm_ms = nbytes / COPY_CEILING * 1e3
-        bound = max(valu_ms, lds_ms, hbm_ms)
-        bound_cf = max(valu_ms, lds_cf_ms, hbm_ms)
-        print(f"{kern},{valu_ms:.3f},{lds_ms:.3f},{lds_cf_ms:.3f},{hbm_ms:.3f},{bound:.3f},{bound_cf:.3f},"
-              f"{meas:.4f},{bound / meas:.3f},{conf / act if act else 0:.3f}")
-    print(f"# target {TARGET_MS} ms (VERDICT r04); a layout is worth building when its bound, with the "
-          "overlap the current kernel achieves, lands below it")
+          "bound_over_measured,conflict_share")
+    for spec in a.steady:
+        sub, f = spec.split("=", 1)
+        k = find(counters, sub)
+        meas, nbytes = steady_ms(f, k)
+        row(k, counters[k], meas, nbytes, rate)
+    for spec in a.compose:
+        label, expr = spec.split("=", 1)
+        c = {}
+        for term in expr.split("+"):
+            sub, w = term.rsplit("*", 1)
+            for name, v in counters[find(counters, sub)].items():
+                c[name] = c.get(name, 0.0) + float(w) * v
+        row(label + " (composed)", c, float("nan"), a.bytes, rate)
+    print(f"# target {TARGET_MS} ms (VERDICT r04). bound = max(valu, lds, hbm): no schedule beats it; "
+          "bound_over_measured is the overlap the kernel achieves. A composed formulation is worth "
+          "building when its bound, at the measured kernels' overlap, lands below the target.")
     return 0
 
 
