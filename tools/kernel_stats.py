@@ -11,7 +11,7 @@ first `--skip` dispatches (bench.py's --warmup) and keeps `--keep` (its
 --steps; default: all remaining).
 
 usage: tools/kernel_stats.py TRACE_DIR_OR_CSV KERNEL_SUBSTRING [--skip W] [--keep K]
-                             [--bytes B] [--out FILE] [--command CMD]
+                             [--bytes B] [--out FILE] [--trace-out FILE] [--command CMD]
 Prints (and writes with --out) a CSV: kernel, dispatches, skipped, kept,
 avg/median/min/max ns of the kept dispatches and, given --bytes (algorithmic
 bytes per launch), the achieved GB/s and the fraction of 8 TB/s.
@@ -44,6 +44,8 @@ def main(argv=None):
     ap.add_argument("--bytes", type=float, default=0.0)
     ap.add_argument("--peak", type=float, default=8000.0, help="GB/s")
     ap.add_argument("--out")
+    ap.add_argument("--trace-out", help="also write every dispatch of the kernel (the rows averaged, and the "
+                                        "warm-up ones marked) as a compact CSV: the evidence behind --out")
     ap.add_argument("--command", default="")
     ap.add_argument("--config", default="", help='e.g. "workload=encode k=10 p=4 len=1048576 stripes=1024" '
                                                  "(bench.py matches its own configuration against it)")
@@ -73,6 +75,17 @@ def main(argv=None):
     if a.out:
         with open(a.out, "w", newline="") as fh:
             csv.writer(fh).writerows(out)
+    if a.trace_out:
+        kept_ids = {id(r) for r in kept}
+        with open(a.trace_out, "w", newline="") as fh:
+            t = csv.writer(fh)
+            t.writerow([f"# per-dispatch rocprofv3 kernel trace of {a.kernel!r} behind "
+                        f"{os.path.basename(a.out) if a.out else 'the summary'}; config: {a.config}"])
+            t.writerow(["dispatch", "start_ns", "end_ns", "duration_ns", "averaged", "kernel"])
+            for r in rows:
+                s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                t.writerow([r.get("Dispatch_Id", ""), s0, e0, e0 - s0, int(id(r) in kept_ids),
+                            r["Kernel_Name"].split("(")[0].replace("void ", "")])
     return 0
 
 
