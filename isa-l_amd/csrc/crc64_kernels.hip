@@ -22,10 +22,10 @@
 namespace {
 
 constexpr int kF = ISAL_HIP_CRC_FIELDS;
-constexpr int kOp = ISAL_HIP_CRC64_OP_ENTRIES;
-constexpr int kKernTab = ISAL_HIP_CRC64_OP_BLOCK - ISAL_HIP_CRC64_CHUNK_TAB;  // chunk + shift
-constexpr int kChunk = 0;                                                        // offsets in LDS copy
-constexpr int kShift = ISAL_HIP_CRC64_SHIFT_TAB - ISAL_HIP_CRC64_CHUNK_TAB;
+[[maybe_unused]] constexpr int kOp = ISAL_HIP_CRC64_OP_ENTRIES;
+[[maybe_unused]] constexpr int kKernTab = ISAL_HIP_CRC64_OP_BLOCK - ISAL_HIP_CRC64_CHUNK_TAB;  // chunk + shift
+[[maybe_unused]] constexpr int kChunk = 0;                                                        // offsets in LDS copy
+[[maybe_unused]] constexpr int kShift = ISAL_HIP_CRC64_SHIFT_TAB - ISAL_HIP_CRC64_CHUNK_TAB;
 
 static_assert(ISAL_HIP_CRC_TILE == kTile, "CRC tile = encode tile");
 static_assert(kF == 7, "field layout below assumes 7 fields per dword");
@@ -142,7 +142,7 @@ __device__ __forceinline__ void load_lds(uint64_t* dst, const uint64_t* __restri
   for (int i = threadIdx.x; i < N / 2; i += kBlock * NV) d[i] = s[i];
 }
 
-constexpr int kCE = ISAL_HIP_CRC64_CHUNK_ENTRIES;
+[[maybe_unused]] constexpr int kCE = ISAL_HIP_CRC64_CHUNK_ENTRIES;
 
 #ifndef ISAL_FUSED64_PART  // standalone kernels: the main object only
 
@@ -385,15 +385,6 @@ __device__ __forceinline__ void byte_offs8(uint32_t w, uint32_t (&o)[4]) {
       : "=v"(o[3]) : "v"(three), "v"(w));
 }
 
-// Bytes 0 and 2 of w times 8.
-__device__ __forceinline__ void byte_offs8(uint32_t w, uint32_t& o0, uint32_t& o2) {
-  const uint32_t three = 3;
-  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
-      : "=v"(o0) : "v"(three), "v"(w));
-  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
-      : "=v"(o2) : "v"(three), "v"(w));
-}
-
 __device__ __forceinline__ uint64_t tab8_at(const uint64_t* t, int j, uint32_t o) {
   return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(t) + j * 2048 + o);
 }
@@ -448,7 +439,7 @@ __device__ __forceinline__ uint64_t tab8_issue(const uint64_t* t, int j, uint32_
   return *(lu64*)((lchar*)(t) + j * 2048 + o);
 }
 
-__device__ __forceinline__ void issue8(Look8& r, const uint64_t* t, uint32_t lo, uint32_t hi) {
+[[maybe_unused]] __device__ __forceinline__ void issue8(Look8& r, const uint64_t* t, uint32_t lo, uint32_t hi) {
   uint32_t o[4], q[4];
   byte_offs8(lo, o);
   byte_offs8(hi, q);
@@ -459,7 +450,7 @@ __device__ __forceinline__ void issue8(Look8& r, const uint64_t* t, uint32_t lo,
   }
 }
 
-__device__ __forceinline__ X64 fold8(const Look8& r) {
+[[maybe_unused]] __device__ __forceinline__ X64 fold8(const Look8& r) {
   X64 a{0u, 0u};
   a.add2(r.v[0], r.v[1]);
   a.add2(r.v[2], r.v[3]);

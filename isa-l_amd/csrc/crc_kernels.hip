@@ -89,7 +89,7 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t chunk_crc(const uint
   return chunk_map(lt + ISAL_HIP_CRC_CHUNK_TAB, w0, w1, w2, w3);
 }
 
-__device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, const uint4& x) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t chunk_crc(const uint32_t* lt, const uint4& x) {
   return chunk_crc(lt, x.x, x.y, x.z, x.w);
 }
 

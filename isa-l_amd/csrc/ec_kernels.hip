@@ -810,27 +810,40 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
 }
 
 // ISAL_HIP_KARG_NARROW: 1 = always the 4-byte-lane kernel, 0 = never;
-// default = shards up to 1 MiB. C2 stripes, same box, two runs each
-// (profiles/r04_karg_narrow_ab.jsonl): 16 threads 3098-3121 -> 3312-3326 GiB/s,
-// 1 thread 18.2 -> 17.9 us per call, 4 KiB shards flat; 4 MiB shards
-// 24.4 -> 27.0 us (4x the load instructions once the call fills the GPU).
-static bool karg_narrow(int len) {
+// default = shards up to 1 MiB while at least kNarrowBusy kernel-argument
+// calls are in flight. Round 4, C2 stripes, synchronised calls, same box
+// (profiles/r04_karg_narrow_ab.jsonl): 16 threads 3098-3121 -> 3312-3326 GiB/s
+// with 4-byte lanes, 1 thread 18.2 -> 17.9 us, 4 MiB shards 24.4 -> 27.0 us
+// (4x the load instructions once one call fills the GPU). Round 5, mailbox
+// completion, two interleaved rounds (profiles/r05/r05_dropin_done_ab.txt):
+// 16-byte lanes are ahead at 1 thread (13.91-14.05 vs 14.50-14.68 us) and 4
+// threads (2867-2895 vs 2730-2849 GiB/s), 4-byte lanes at 16 threads
+// (4077-4098 vs 4019-4035 GiB/s). Choosing by calls in flight, two rounds
+// (profiles/r05/r05_dropin_width_ab.txt): 1 thread 13.74-13.80 us, 16 threads
+// 4079-4101 GiB/s; at 8 threads 16-byte lanes led (3884-3931 vs 3790-3830
+// GiB/s), so 4-byte lanes start at 12 calls in flight (16 threads keep
+// 14-16 in flight).
+constexpr int kNarrowBusy = 12;
+static bool karg_narrow(int len, int busy) {
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_KARG_NARROW);
   if (v >= 0) return v != 0;
-  return len <= (1 << 20);
+  return len <= (1 << 20) && busy >= kNarrowBusy;
 }
 
 static const isal_hip_kdone kNoDone = {nullptr, nullptr, nullptr, 0ull};
 
 extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, const isal_hip_kdone* d, int len, int k,
-                                           int rows, const isal_hip_encmask* em, void* stream) {
+                                           int rows, const isal_hip_encmask* em, int busy, void* stream) {
   if (!d) d = &kNoDone;
   if (len <= 0 || rows <= 0) return 0;
   if (rows > EC_MAX_ROWS_PER_PASS || k + rows > ISAL_HIP_KARG_PTRS ||
       static_cast<size_t>(kTbl) * k * rows > ISAL_HIP_KARG_TBL)
     return static_cast<int>(hipErrorInvalidValue);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (karg_narrow(len)) {
+  const bool narrow = karg_narrow(len, busy);
+  if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2)
+    fprintf(stderr, "isal_hip: kernel %s<%d>\n", narrow ? "ec_encode_karg4" : "ec_encode_karg", rows);
+  if (narrow) {
     const unsigned blocks = static_cast<unsigned>((static_cast<long long>(len) + 4 * kBlock - 1) / (4 * kBlock));
     switch (rows) {
 #define EC_KARG4(n)                                                                                           \

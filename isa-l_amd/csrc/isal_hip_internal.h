@@ -74,13 +74,14 @@ typedef struct {
         uint32_t tbl[ISAL_HIP_KARG_TBL];
 } isal_hip_karg;
 /* Completion of a kernel-argument call without the runtime's wake-up: every
- * workgroup publishes its stores (agent-scope release) and counts itself in
- * *cnt; the last one resets *cnt (and *res) for the next call and writes
- * mail[1] = the verify result (*res, ~0 for encode / update), then mail[0] =
- * seq (system-scope release) into page-locked host memory that the calling
- * thread spins on (isal_hip_shim.c wait_done). cnt = NULL: no protocol (the
- * caller synchronises the stream). res: device word a verify's mismatching
- * lanes atomically lower (~0 between calls); NULL for encode / update. */
+ * workgroup waits for its (write-through) stores and counts itself in *cnt;
+ * the last one resets *cnt (and *res) for the next call and writes mail[1] =
+ * the verify result (*res, ~0 for encode / update), then mail[0] = seq
+ * (system-scope stores) into page-locked host memory that the calling thread
+ * spins on (isal_hip_shim.c wait_done; ec_kernels.hip karg_done). cnt = NULL:
+ * no protocol (the caller synchronises the stream). res: device word a
+ * verify's mismatching lanes atomically lower (~0 between calls); NULL for
+ * encode / update. */
 typedef struct {
         unsigned *cnt;
         unsigned long long *res;
@@ -95,8 +96,10 @@ typedef struct {
 #define ISAL_HIP_KDONE_GROUPS 256
 #define ISAL_HIP_KDONE_STRIDE 16
 #define ISAL_HIP_KDONE_WORDS ((ISAL_HIP_KDONE_GROUPS + 1) * ISAL_HIP_KDONE_STRIDE)
+/* busy: kernel-argument calls of this process in flight, this one included
+ * (chooses the lane width, ec_kernels.hip karg_narrow). */
 int isal_hip_launch_encode_karg(const isal_hip_karg *a, const isal_hip_kdone *d, int len, int k, int rows,
-                                const isal_hip_encmask *em, void *stream);
+                                const isal_hip_encmask *em, int busy, void *stream);
 /* ec_encode_data_update of one stripe the same way: ptrs = {source, rows
  * parity}, tbl = the source's tables for rows <= EC_MAX_ROWS_PER_PASS outputs. */
 int isal_hip_launch_update_karg(const isal_hip_karg *a, const isal_hip_kdone *d, int len, int rows,

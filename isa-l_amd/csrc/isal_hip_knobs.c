@@ -7,7 +7,7 @@
  * reference has no runtime configuration beyond its CPU dispatch (SURVEY.md
  * §5 "Config / flags"); these knobs are the engine's own. Round 5 removed the
  * 18 that only selected variants measured flat or slower (their A/B results
- * stay in DESIGN.md §7): every knob left either switches a default-on
+ * stay in DESIGN.md §2b): every knob left either switches a default-on
  * mechanism off for an A/B or a fallback, or exists for a test.
  */
 #include <pthread.h>

@@ -1502,11 +1502,13 @@ static gpu_res
 gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *view, const uint32_t *tbl,
          const isal_hip_encmask *em, int mail)
 {
+        static int inflight; /* kernel-argument calls of the process in flight (lane width) */
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         const int nsrc = op == OP_UPDATE ? 1 : k;
         isal_hip_kdone d = {NULL, NULL, NULL, 0ull};
         isal_hip_karg a;
-        hipError_t e;
+        hipError_t e, w;
+        int busy;
         memset(&a, 0, sizeof(a));
         memcpy(a.ptrs, view, sizeof(uint64_t) * (size_t) (nsrc + rows));
         if (mail) {
@@ -1522,11 +1524,20 @@ gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *
                 e = (hipError_t) isal_hip_launch_update_karg(&a, &d, len, rows, c->stream);
         } else {
                 memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
-                e = (hipError_t) (op == OP_VERIFY ? isal_hip_launch_verify_karg(&a, &d, len, k, rows, em, c->stream)
-                                                  : isal_hip_launch_encode_karg(&a, &d, len, k, rows, em, c->stream));
+                busy = __atomic_add_fetch(&inflight, 1, __ATOMIC_RELAXED);
+                e = (hipError_t) (op == OP_VERIFY
+                                          ? isal_hip_launch_verify_karg(&a, &d, len, k, rows, em, c->stream)
+                                          : isal_hip_launch_encode_karg(&a, &d, len, k, rows, em, busy, c->stream));
+                if (e != hipSuccess)
+                        __atomic_sub_fetch(&inflight, 1, __ATOMIC_RELAXED);
         }
         GPU_TRY_AT(r, FAULT_LAUNCH, e);
-        GPU_TRY_AT(r, FAULT_SYNC, mail ? wait_done(c, d.seq) : hipStreamSynchronize(c->stream));
+        w = fault_at(FAULT_SYNC, 0) ? hipErrorOutOfMemory
+            : mail                  ? wait_done(c, d.seq)
+                                    : hipStreamSynchronize(c->stream);
+        if (op != OP_UPDATE)
+                __atomic_sub_fetch(&inflight, 1, __ATOMIC_RELAXED);
+        GPU_TRY_AT(r, FAULT_SYNC, w);
         if (op == OP_VERIFY)
                 r.first_bad = c->h_mail[1];
         r.done = len;

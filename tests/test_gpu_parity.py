@@ -41,7 +41,10 @@ def _reload_knobs_after(engine):
 def _setenv(monkeypatch, name, value):
     import isal_amd
 
-    monkeypatch.setenv(name, value)
+    if value is None:  # back to the library's default
+        monkeypatch.delenv(name, raising=False)
+    else:
+        monkeypatch.setenv(name, value)
     isal_amd.reload_config()
 
 
@@ -451,8 +454,7 @@ def test_encode_load_groups_vs_oracle(engine, oracle, gpu, monkeypatch, glds, k,
     b.close()
 
 
-@pytest.mark.parametrize("narrow", ["1", "0"])
-@pytest.mark.parametrize("k,rows,n", [
+_KARG_SHAPES = [
     (10, 4, 1 << 20),      # C2 stripe
     (10, 4, 16),           # shortest kernel-argument call: one lane
     (10, 4, 4096 * 3 + 7), # ragged tail: 3 bytes past the last full lane dword
@@ -461,17 +463,27 @@ def test_encode_load_groups_vs_oracle(engine, oracle, gpu, monkeypatch, glds, k,
     (10, 8, 4096 + 4),     # 8 rows
     (1, 1, 64),
     (14, 6, 20000),        # 5 * k * rows = 420 of the 448 table dwords
+]
+
+
+@pytest.mark.parametrize("narrow,k,rows,n", [(w,) + s for w in ("1", "0") for s in _KARG_SHAPES] + [
+    ("", 10, 4, 1 << 20),         # default threshold: the last 4-byte-lane size
+    ("", 10, 4, (1 << 20) + 16),  # one lane past it: the 16-byte-lane kernel
 ])
 def test_dropin_kernel_args_vs_oracle(engine, oracle, gpu, monkeypatch, capfd, narrow, k, rows, n):
     """The drop-in call on 16-byte-aligned device shards passes its pointers and
     tables as kernel arguments; its kernel takes 16 bytes per lane or, with
-    ISAL_HIP_KARG_NARROW (default for shards up to 4 MiB), 4 bytes per lane:
-    both == oracle, tails included, and the route log names the route."""
+    ISAL_HIP_KARG_NARROW (default for shards up to 1 MiB while at least 12
+    such calls are in flight), 4 bytes per lane: both == oracle, tails
+    included, and the route log names the route and the kernel. narrow "" is
+    the default: a lone call takes the 16-byte-lane kernel at 1 MiB and at
+    1 MiB + 16 (test_dropin_lane_width_follows_concurrency covers the
+    concurrent side)."""
     import torch
 
     _setenv(monkeypatch, "ISAL_HIP_BACKEND", "gpu")
-    _setenv(monkeypatch, "ISAL_HIP_KARG_NARROW", narrow)
-    _setenv(monkeypatch, "ISAL_HIP_LOG", "1")
+    _setenv(monkeypatch, "ISAL_HIP_KARG_NARROW", narrow or None)
+    _setenv(monkeypatch, "ISAL_HIP_LOG", "2")
     coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:] if rows > 1 else np.full(k, 3, dtype=np.uint8)
     tbls = engine.ec_init_tables(k, rows, coef)
     stride = (n + 15) // 16 * 16 + 256
@@ -485,12 +497,36 @@ def test_dropin_kernel_args_vs_oracle(engine, oracle, gpu, monkeypatch, capfd, n
     capfd.readouterr()
     engine.ec_encode_data(n, k, rows, tbls, [shard(j) for j in range(k)], [shard(k + l) for l in range(rows)])
     torch.cuda.synchronize()
-    assert "kernel-args" in capfd.readouterr().err
+    err = capfd.readouterr().err
+    assert "kernel-args" in err
+    four = narrow == "1"  # default, one call in flight: 16-byte lanes
+    assert f"kernel {'ec_encode_karg4' if four else 'ec_encode_karg'}<{rows}>" in err, err
     out = _host(buf)
     for l in range(rows):
         base = (k + l) * stride
         assert np.array_equal(out[base: base + n], want[l]), l
         assert np.array_equal(out[base + n: base + stride], canary[l * stride + n: (l + 1) * stride]), l
+
+
+def test_dropin_lane_width_follows_concurrency(gpu):
+    """Default lane width of the drop-in encode (ec_kernels.hip karg_narrow):
+    16-byte lanes while fewer than 12 kernel-argument calls are in flight,
+    4-byte lanes from 12 on. tools/dropin_bench (C threads, no GIL between
+    calls) runs 16 threads of 200 calls each with the kernel log on: both
+    kernels must appear, the first (warm-up, one thread) call must be the
+    16-byte one, and the run's own parity self-check must pass."""
+    exe = os.path.join(ecutil.REPO, "tools", "dropin_bench")
+    if not os.path.exists(exe):
+        pytest.fail("tools/dropin_bench not built (make -C isa-l_amd tools)")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ISAL_HIP_")}
+    env["ISAL_HIP_LOG"] = "2"
+    r = subprocess.run([exe, "10", "4", "65536", "64", "16", "0", "200"], capture_output=True, text=True,
+                       env=env, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert '"self_check": true' in r.stdout, r.stdout
+    kern = [l.split("kernel ", 1)[1] for l in r.stderr.splitlines() if l.startswith("isal_hip: kernel ec_encode_karg")]
+    assert kern and kern[0] == "ec_encode_karg<4>", kern[:4]
+    assert "ec_encode_karg4<4>" in kern, "16 concurrent callers never took the 4-byte-lane kernel"
 
 
 def test_config_c1_cauchy_k4_p2_64k(engine, gpu):
@@ -1369,9 +1405,12 @@ CONFORMANCE = ["gf_inverse_test", "gf_vect_mul_test", "gf_vect_mul_base_test",
 
 
 # xor_check_test / pq_check_test sweep every (length, error position, vector)
-# with ~1.6e7 small synchronous calls each: at a ~30 us GPU round trip per call
-# that is ~10 minutes apiece, so under ISAL_HIP_BACKEND=gpu they run only with
-# ISAL_SLOW_CONFORMANCE=1 (logs: profiles/r01/r01_slow_conformance_*.log). Under
+# with 1.65e7 / 1.20e7 small synchronous calls (counted from ISAL_HIP_LOG=1
+# route lines): forced onto the GPU a 17-buffer 1 KiB call costs 22 us
+# (xor_check) / 34 us (pq_check) on pageable memory
+# (profiles/r05/r05_raid_small_calls.txt), ~6-7 minutes apiece, so under
+# ISAL_HIP_BACKEND=gpu they run only with ISAL_SLOW_CONFORMANCE=1 (logs:
+# profiles/r05/r05_slow_conformance.txt, r01/r01_slow_conformance_*.log). Under
 # the library's default routing (auto: small host calls on the CPU route, the
 # rest on the GPU) all thirteen run.
 SLOW_CONFORMANCE = {"xor_check_test", "pq_check_test"}

@@ -32,7 +32,90 @@ __global__ __launch_bounds__(kBlock) void copy_tiles(uint64_t dst, uint64_t src,
   __builtin_amdgcn_raw_buffer_store_b128(v, rd, off, 0, 2 /* nt */);
 }
 
+// The memory skeleton of one encode shape: K source shards read and P output
+// shards written per stripe, 16 bytes per lane per shard, one 4 KiB column tile
+// per workgroup, tiles of a stripe consecutive and the (stripe, tile) items
+// handed out XCD-contiguously (the encode's EncOrder<2>), nt buffer loads and
+// stores — the encode with its GF arithmetic replaced by one XOR fold. P = 0 is
+// a read-only pass (the check kernels' shape). Layout as bench.py allocates it:
+// data[S][K][len], coding[S][P][len].
+template <int K, int P>
+__global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t coding, int len, unsigned tiles,
+                                                     unsigned nitems) {
+  extern __shared__ unsigned lds_pad[];  // the encode's occupancy cap (dynamic LDS), unused
+  const unsigned per = nitems / 8;
+  const unsigned w = blockIdx.x;
+  const unsigned item = (nitems % 8) ? w : (w % 8) * per + w / 8;
+  const unsigned s = item / tiles, t = item % tiles;
+  const int off = static_cast<int>(t) * kTile + threadIdx.x * 16;
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  v4i v[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(data + (static_cast<uint64_t>(s) * K + j) * static_cast<uint64_t>(len)), 0, len,
+        0x00020000);
+    v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2 /* nt */);
+  }
+  v4i acc = v[0];
+#pragma unroll
+  for (int j = 1; j < K; ++j) acc ^= v[j];
+  if (P == 0) {
+    if (acc.x == 0x7eadbeef && acc.y == 0x1234567 && acc.z == 0x89abcdef && acc.w == 0x0f1e2d3c) lds_pad[0] = 1;
+    return;
+  }
+#pragma unroll
+  for (int l = 0; l < P; ++l) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(coding + (static_cast<uint64_t>(s) * P + l) * static_cast<uint64_t>(len)), 0,
+        len, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(acc ^ l, r, off, 0, 2 /* nt */);
+  }
+}
+
 }  // namespace
+
+// Runs the (K, P) skeleton over S stripes of len-byte shards `reps` times after
+// two warm-ups with `lds` bytes of dynamic LDS per workgroup; returns the
+// rate in GB/s of (K + P) * len * S bytes per pass, or a negative error.
+extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p, unsigned stripes, int reps,
+                                 unsigned lds) {
+  if (len <= 0 || len % kTile || reps <= 0 || stripes == 0) return -1.0;
+  const unsigned tiles = static_cast<unsigned>(len / kTile), nitems = tiles * stripes;
+  void (*kern)(uint64_t, uint64_t, int, unsigned, unsigned) = nullptr;
+  switch (k * 100 + p) {
+    case 101: kern = skel_tiles<1, 1>; break;
+    case 1004: kern = skel_tiles<10, 4>; break;
+    case 1000: kern = skel_tiles<10, 0>; break;
+    case 1200: kern = skel_tiles<12, 0>; break;
+    case 1002: kern = skel_tiles<10, 2>; break;
+    case 1006: kern = skel_tiles<10, 6>; break;
+    case 1008: kern = skel_tiles<10, 8>; break;
+    case 2006: kern = skel_tiles<20, 6>; break;
+    case 2008: kern = skel_tiles<20, 8>; break;
+    case 1003: kern = skel_tiles<10, 3>; break;
+    default: return -4.0;
+  }
+  hipStream_t st;
+  hipEvent_t e0, e1;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return -2.0;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int i = 0; i < reps + 2; ++i) {
+    if (i == 2) (void)hipEventRecord(e0, st);
+    hipLaunchKernelGGL(kern, dim3(nitems), dim3(kBlock), lds, st, reinterpret_cast<uint64_t>(data),
+                       reinterpret_cast<uint64_t>(coding), len, tiles, nitems);
+  }
+  (void)hipEventRecord(e1, st);
+  const hipError_t err = hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(st);
+  if (err != hipSuccess || ms <= 0.f) return -3.0;
+  return static_cast<double>(k + p) * len * stripes * reps / (ms * 1e-3) / 1e9;
+}
 
 // Copies n bytes (a multiple of 4 KiB, at most 2^40) from src to dst `reps`
 // times after two warm-up copies, on a stream of its own; returns the copy

@@ -20,6 +20,11 @@
  * wall / calls per thread), calls/s and GiB/s of (K+P)*LEN per call (the
  * reference's perf_print convention, erasure_code_perf.c:304).
  *
+ * DROPIN_MEM=host|pinned puts the stripes in pageable malloc memory or
+ * hipHostMalloc memory instead of HBM (with ISAL_HIP_BACKEND=gpu: the per-call
+ * cost of the reference's own tests forced onto the kernels, e.g.
+ * raid/xor_check_test.c's 1 KiB calls over 17 host buffers).
+ *
  * Self-check (no oracle): for the first and last stripe, 8192 sampled columns
  * of every parity row are recomputed on the host from the library's host GF
  * math (gf_mul of the generator matrix, itself pinned by the reference's
@@ -41,6 +46,19 @@
 enum { OP_ENCODE, OP_PQ_GEN, OP_XOR_GEN, OP_PQ_CHECK, OP_XOR_CHECK };
 static const char *const op_names[] = {"encode", "pq_gen", "xor_gen", "pq_check", "xor_check", NULL};
 static int g_op = OP_ENCODE;
+enum { MEM_DEVICE, MEM_HOST, MEM_PINNED };
+static int g_mem = MEM_DEVICE;
+
+/* stripes in host memory are copied by the CPU; in HBM through
+ * hipMemcpyDefault (the runtime infers the direction from the pointers) */
+static void
+copy(void *dst, const void *src, size_t n)
+{
+        if (g_mem != MEM_DEVICE)
+                memcpy(dst, src, n);
+        else
+                (void) hipMemcpy(dst, src, n, hipMemcpyDefault);
+}
 static long long g_check_fail;
 
 static double
@@ -145,9 +163,9 @@ check_stripe(const worker_t *w, const unsigned char *a, int s)
         if (!src || !par)
                 return 1;
         for (i = 0; i < k; i++)
-                (void) hipMemcpy(src + (size_t) i * len, shard(w, s, i), (size_t) len, hipMemcpyDeviceToHost);
+                copy(src + (size_t) i * len, shard(w, s, i), (size_t) len);
         for (l = 0; l < p; l++)
-                (void) hipMemcpy(par + (size_t) l * len, shard(w, s, k + l), (size_t) len, hipMemcpyDeviceToHost);
+                copy(par + (size_t) l * len, shard(w, s, k + l), (size_t) len);
         for (c = 0; c < ncol && !bad; c++) {
                 int col;
                 x ^= x << 13;
@@ -184,7 +202,7 @@ main(int argc, char **argv)
         hipError_t e;
 
         if (argc < 7) {
-                fprintf(stderr, "usage: %s K P LEN STRIPES THREADS SECONDS [CALLS_PER_THREAD]\n", argv[0]);
+                fprintf(stderr, "usage: %s K P LEN STRIPES THREADS SECONDS [CALLS_PER_THREAD [OP]]\n", argv[0]);
                 return 2;
         }
         k = atoi(argv[1]);
@@ -213,8 +231,14 @@ main(int argc, char **argv)
         if (stripes < nthreads)
                 stripes = nthreads;
         total = (size_t) stripes * (size_t) (k + p) * (size_t) len;
-        if ((e = hipMalloc((void **) &base, total)) != hipSuccess) {
-                fprintf(stderr, "dropin_bench: hipMalloc(%zu): %s\n", total, hipGetErrorString(e));
+        if (getenv("DROPIN_MEM"))
+                g_mem = !strcmp(getenv("DROPIN_MEM"), "host") ? MEM_HOST
+                        : !strcmp(getenv("DROPIN_MEM"), "pinned") ? MEM_PINNED : MEM_DEVICE;
+        e = g_mem == MEM_DEVICE ? hipMalloc((void **) &base, total)
+            : g_mem == MEM_PINNED ? hipHostMalloc((void **) &base, total, 0)
+            : (base = aligned_alloc(64, (total + 63) / 64 * 64)) ? hipSuccess : hipErrorOutOfMemory;
+        if (e != hipSuccess) {
+                fprintf(stderr, "dropin_bench: allocation of %zu bytes: %s\n", total, hipGetErrorString(e));
                 return 1;
         }
         /* sources random, parity zero; one host stripe of random bytes copied
@@ -229,16 +253,20 @@ main(int argc, char **argv)
                 x ^= x << 17;
                 h[b] = (unsigned char) (x >> 32);
         }
-        (void) hipMemset(base, 0, total);
+        if (g_mem == MEM_DEVICE)
+                (void) hipMemset(base, 0, total);
+        else
+                memset(base, 0, total);
         for (i = 0; i < stripes; i++) {
                 const size_t rot = ((size_t) i * 977) % nsrc_bytes;
                 unsigned char *dst = base + (size_t) i * (size_t) (k + p) * (size_t) len;
-                (void) hipMemcpy(dst, h + rot, nsrc_bytes - rot, hipMemcpyHostToDevice);
+                copy(dst, h + rot, nsrc_bytes - rot);
                 if (rot)
-                        (void) hipMemcpy(dst + nsrc_bytes - rot, h, rot, hipMemcpyHostToDevice);
+                        copy(dst + nsrc_bytes - rot, h, rot);
         }
         free(h);
-        (void) hipDeviceSynchronize();
+        if (g_mem == MEM_DEVICE)
+                (void) hipDeviceSynchronize();
 
         a = malloc((size_t) (k + p) * (size_t) k);
         tbls = malloc((size_t) 32 * (size_t) k * (size_t) p);
@@ -296,22 +324,27 @@ main(int argc, char **argv)
         if (ok && (g_op == OP_PQ_CHECK || g_op == OP_XOR_CHECK)) {
                 /* one corrupted byte in the middle of source 1 of stripe 0 must be reported */
                 unsigned char *b = shard(&w[0], 0, 1) + len / 2, v;
-                (void) hipMemcpy(&v, b, 1, hipMemcpyDeviceToHost);
+                copy(&v, b, 1);
                 v ^= 0x08;
-                (void) hipMemcpy(b, &v, 1, hipMemcpyHostToDevice);
+                copy(b, &v, 1);
                 if (call_op(&w[0], 0) == 0) {
                         fprintf(stderr, "dropin_bench: corrupted stripe not reported\n");
                         ok = 0;
                 }
                 v ^= 0x08;
-                (void) hipMemcpy(b, &v, 1, hipMemcpyHostToDevice);
+                copy(b, &v, 1);
         }
-        printf("{\"op\": \"%s\", \"k\": %d, \"p\": %d, \"len\": %d, \"stripes\": %d, \"threads\": %d, \"calls\": %lld, "
+        printf("{\"op\": \"%s\", \"k\": %d, \"p\": %d, \"len\": %d, \"stripes\": %d, \"threads\": %d, \"mem\": \"%s\", \"calls\": %lld, "
                "\"wall_s\": %.4f, \"us_per_call\": %.2f, \"calls_per_s\": %.1f, \"gib_s\": %.3f, "
                "\"first_timed_call_us_thread0\": %.1f, \"self_check\": %s}\n",
-               op_names[g_op], k, p, len, stripes, nthreads, calls, wall, wall / ((double) calls / nthreads) * 1e6,
+               op_names[g_op], k, p, len, stripes, nthreads, g_mem == MEM_DEVICE ? "device" : g_mem == MEM_HOST ? "host" : "pinned", calls, wall, wall / ((double) calls / nthreads) * 1e6,
                (double) calls / wall, (double) calls * (double) (k + p) * (double) len / wall / (double) (1 << 30),
                w[0].first_call_us, ok ? "true" : "false");
-        (void) hipFree(base);
+        if (g_mem == MEM_DEVICE)
+                (void) hipFree(base);
+        else if (g_mem == MEM_PINNED)
+                (void) hipHostFree(base);
+        else
+                free(base);
         return ok ? 0 : 1;
 }

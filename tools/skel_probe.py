@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""The memory skeleton of each encode shape as its own ceiling (DESIGN.md §3,
+"What bounds each encode shape"): tools/copy_probe.hip:skel_tiles reads K
+source shards and writes P output shards per stripe exactly as the encode
+does (16 B per lane, 4 KiB column tiles, XCD-contiguous items, nt buffer
+loads/stores) with the GF arithmetic replaced by one XOR fold. Prints one JSON
+line per (shape, LDS cap): GB/s of (K+P)*len*S per pass and the fraction of
+8 TB/s. Run on the GPU box: python3 tools/skel_probe.py [REPS]
+"""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MiB = 1 << 20
+SHAPES = [  # (label, k, p, len, stripes)
+    ("copy 1:1", 1, 1, MiB, 4096),
+    ("C2 encode k10p4", 10, 4, MiB, 1024),
+    ("C3 decode k10 -> 3", 10, 3, MiB, 1024),
+    ("pq_gen k10p2", 10, 2, MiB, 1024),
+    ("k10p6", 10, 6, MiB, 1024),
+    ("k10p8", 10, 8, MiB, 1024),
+    ("k20p6", 20, 6, 4 * MiB, 64),
+    ("k20p8", 20, 8, 4 * MiB, 64),
+    ("read-only k10", 10, 0, MiB, 1024),
+    ("read-only k12 (pq_check)", 12, 0, MiB, 1024),
+]
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    lib = ctypes.CDLL(os.path.join(REPO, "tools", "libcopy_probe.so"))
+    lib.skel_probe_gbs.restype = ctypes.c_double
+    lib.skel_probe_gbs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_uint, ctypes.c_int, ctypes.c_uint]
+    data = torch.empty(12 << 30, dtype=torch.uint8, device="cuda")
+    data.view(torch.int32).random_()
+    coding = torch.empty(8 << 30, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    for label, k, p, n, s in SHAPES:
+        assert k * n * s <= data.numel() and p * n * s <= coding.numel()
+        for lds in (0, 32768):
+            g = lib.skel_probe_gbs(data.data_ptr(), coding.data_ptr(), n, k, p, s, reps, lds)
+            print(json.dumps({"shape": label, "k": k, "p": p, "len": n, "stripes": s, "lds_bytes": lds,
+                              "reps": reps, "gb_s": round(g, 1), "frac_of_8tbs": round(g / 8000.0, 4)}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
