@@ -1,5 +1,6 @@
 # Final-tree bench lines for every workload (headline with the CPU baseline on
-# the usable cores), and rocprof traces + HBM traffic of the RAID kernels.
+# the usable cores), the encode memory skeletons on the same box, and rocprof
+# traces + HBM traffic of the RAID kernels.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -7,6 +8,7 @@ O=gpurun_out/r05m; mkdir -p $O
 B="python3 bench.py"
 timeout -k 10 600 $B > $O/bench_c2.json 2> $O/bench_c2.err || { echo FAIL c2; tail $O/bench_c2.err; exit 1; }
 cat $O/bench_c2.json
+timeout -k 10 300 python3 tools/skel_probe.py 10 > $O/skel_probe.jsonl 2> $O/skel_probe.err || { echo SKEL FAIL; tail $O/skel_probe.err; exit 1; }
 while read name args; do
   timeout -k 10 300 $B --no-cpu-baseline $args > $O/bench_$name.json 2> $O/bench_$name.err || { echo FAIL $name; tail $O/bench_$name.err; exit 1; }
 done <<'LIST'
