@@ -56,3 +56,32 @@ def test_erasure_sets_rotate_and_stay_in_range():
         seen.update(e)
     assert seen == set(range(k))
     assert bench.erasure_set(3, 5, 0) == [0, 1, 2]
+
+
+def test_cpu_baseline_cores_spread_over_l3_domains(monkeypatch):
+    """The CPU baseline pins one thread per physical core, round-robin over
+    the L3 domains (tools/cpu_ref_baseline.py _physical_cpus): on a host of
+    two CCDs x 4 cores with SMT siblings, 4 cores are two per CCD, never a
+    sibling of another chosen CPU; the usable count is capped by the cgroup
+    quota."""
+    sys.path.insert(0, os.path.join(ecutil.REPO, "tools"))
+    import cpu_ref_baseline as crb
+
+    # CPUs 0-7: CCD 0 cores 0-3 and CCD 1 cores 4-7; CPUs 8-15 their siblings
+    def fake_read(path):
+        cpu = int(path.split("/cpu/cpu")[1].split("/")[0])
+        core = cpu % 8
+        if path.endswith("thread_siblings_list"):
+            return f"{core},{core + 8}"
+        if path.endswith("index3/shared_cpu_list"):
+            return "0-3,8-11" if core < 4 else "4-7,12-15"
+        return None
+
+    monkeypatch.setattr(crb, "_read", fake_read)
+    monkeypatch.setattr(crb.os, "sched_getaffinity", lambda pid: set(range(16)))
+    assert crb._physical_cpus(4) == [0, 4, 1, 5]
+    assert sorted(crb._physical_cpus(0)) == list(range(8))
+    monkeypatch.setattr(crb, "cgroup_cpu_quota", lambda: 3.0)
+    assert crb.usable_cores() == 3
+    monkeypatch.setattr(crb, "cgroup_cpu_quota", lambda: None)
+    assert crb.usable_cores() == 8
