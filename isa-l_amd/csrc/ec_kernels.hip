@@ -376,11 +376,21 @@ __device__ __forceinline__ void verify_items(const uint64_t* __restrict__ ptrs, 
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec <= len) {
+      // Up to 3 rows (RAID P / P+Q, the drop-in xor_check / pq_check) the
+      // stored rows are loaded before the sources' fold, so their latency
+      // overlaps it instead of following it: one HBM round trip less per
+      // tile. Wider passes would spill the extra 4 VGPRs per row.
+      constexpr bool kEarly = P <= 3;
+      uint4 st[kEarly ? P : 1];
+      if constexpr (kEarly) {
+#pragma unroll
+        for (int l = 0; l < P; ++l) st[l] = load16<kBufNT>(sp[dst0 + l], off, len);
+      }
       uint32_t acc[P][4];
       accum16<P, Pol, FL>(acc, sp + src0, tbl, k, off, len, r0m, c0m);
 #pragma unroll
       for (int l = 0; l < P; ++l) {
-        const uint4 e = load16<kBufNT>(sp[dst0 + l], off, len);
+        const uint4 e = kEarly ? st[kEarly ? l : 0] : load16<kBufNT>(sp[dst0 + l], off, len);
         const uint32_t x[4] = {acc[l][0] ^ e.x, acc[l][1] ^ e.y, acc[l][2] ^ e.z, acc[l][3] ^ e.w};
 #pragma unroll
         for (int d = 0; d < 4; ++d)

@@ -94,6 +94,7 @@ extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p
     case 2006: kern = skel_tiles<20, 6>; break;
     case 2008: kern = skel_tiles<20, 8>; break;
     case 1003: kern = skel_tiles<10, 3>; break;
+    case 706: kern = skel_tiles<7, 6>; break;  // C4 update: 1 source + 6 parity read, 6 parity written
     default: return -4.0;
   }
   hipStream_t st;

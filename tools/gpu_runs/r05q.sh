@@ -1,5 +1,5 @@
 # Headline bench with the CPU baselines pinned round-robin over L3 domains
-# (twice), plus the spread's topology.
+# (twice), plus the spread's topology; memory skeletons incl. the update shape.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -8,6 +8,7 @@ python3 -c "import sys; sys.path.insert(0,'tools'); import cpu_ref_baseline as c
 for i in 1 2; do
   timeout -k 10 600 python3 bench.py > $O/bench_c2_$i.json 2> $O/bench_c2_$i.err || { echo FAIL c2; tail $O/bench_c2_$i.err; exit 1; }
 done
+timeout -k 10 300 python3 tools/skel_probe.py 10 > $O/skel_probe.jsonl 2> $O/skel_probe.err || { echo SKEL FAIL; tail $O/skel_probe.err; exit 1; }
 cat $O/cpus.txt
 for i in 1 2; do python3 -c "
 import json; d=json.loads(open('$O/bench_c2_$i.json').read().strip().splitlines()[-1])

@@ -25,6 +25,7 @@ SHAPES = [  # (label, k, p, len, stripes)
     ("k10p8", 10, 8, MiB, 1024),
     ("k20p6", 20, 6, 4 * MiB, 64),
     ("k20p8", 20, 8, 4 * MiB, 64),
+    ("C4 update k20p6 (7 read, 6 written)", 7, 6, 4 * MiB, 64),
     ("read-only k10", 10, 0, MiB, 1024),
     ("read-only k12 (pq_check)", 12, 0, MiB, 1024),
 ]
