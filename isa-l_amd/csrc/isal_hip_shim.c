@@ -1507,7 +1507,7 @@ gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *
         const int nsrc = op == OP_UPDATE ? 1 : k;
         isal_hip_kdone d = {NULL, NULL, NULL, 0ull};
         isal_hip_karg a;
-        hipError_t e, w;
+        hipError_t karg_launch, karg_wait;
         int busy;
         memset(&a, 0, sizeof(a));
         memcpy(a.ptrs, view, sizeof(uint64_t) * (size_t) (nsrc + rows));
@@ -1521,23 +1521,24 @@ gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *
         if (op == OP_UPDATE) {
                 /* one pass: source vec_i's tables for every row are contiguous */
                 memcpy(a.tbl, tbl + isal_hip_tables_dwords(vec_i, rows), isal_hip_tables_dwords(1, rows) * 4);
-                e = (hipError_t) isal_hip_launch_update_karg(&a, &d, len, rows, c->stream);
+                karg_launch = (hipError_t) isal_hip_launch_update_karg(&a, &d, len, rows, c->stream);
         } else {
                 memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
                 busy = __atomic_add_fetch(&inflight, 1, __ATOMIC_RELAXED);
-                e = (hipError_t) (op == OP_VERIFY
+                karg_launch = (hipError_t) (op == OP_VERIFY
                                           ? isal_hip_launch_verify_karg(&a, &d, len, k, rows, em, c->stream)
                                           : isal_hip_launch_encode_karg(&a, &d, len, k, rows, em, busy, c->stream));
-                if (e != hipSuccess)
-                        __atomic_sub_fetch(&inflight, 1, __ATOMIC_RELAXED);
         }
-        GPU_TRY_AT(r, FAULT_LAUNCH, e);
-        w = fault_at(FAULT_SYNC, 0) ? hipErrorOutOfMemory
-            : mail                  ? wait_done(c, d.seq)
-                                    : hipStreamSynchronize(c->stream);
-        if (op != OP_UPDATE)
+        if (karg_launch == hipSuccess && fault_at(FAULT_LAUNCH, 0))
+                karg_launch = hipErrorOutOfMemory; /* injected (tests) */
+        karg_wait = karg_launch != hipSuccess ? karg_launch
+                    : fault_at(FAULT_SYNC, 0) ? hipErrorOutOfMemory
+                    : mail                    ? wait_done(c, d.seq)
+                                              : hipStreamSynchronize(c->stream);
+        if (op != OP_UPDATE) /* this call is no longer in flight, whatever failed */
                 __atomic_sub_fetch(&inflight, 1, __ATOMIC_RELAXED);
-        GPU_TRY_AT(r, FAULT_SYNC, w);
+        GPU_TRY(r, karg_launch);
+        GPU_TRY(r, karg_wait);
         if (op == OP_VERIFY)
                 r.first_bad = c->h_mail[1];
         r.done = len;
