@@ -42,7 +42,7 @@ struct Arg {
 
 template <int N>
 __global__ void __launch_bounds__(256) probe(Arg<N> a, unsigned* cnt, unsigned long long* mail,
-                                             unsigned long long seq, int mode) {
+                                             unsigned long long seq, int mode, unsigned gmin) {
   // every lane reads one argument dword (the kernel-argument traffic of a real call)
   const unsigned v = a.w[threadIdx.x % (N / 4)];
   __syncthreads();
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(256) probe(Arg<N> a, unsigned* cnt, unsigned l
     }
     return;
   }
-  const unsigned gsz = max(32u, (n + kGroups - 1) / kGroups);
+  const unsigned gsz = max(gmin, (n + kGroups - 1) / kGroups);
   const unsigned g = b / gsz, gn = min(gsz, n - g * gsz), ng = (n + gsz - 1) / gsz;
   unsigned* gc = cnt + g * kStride;
   if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gn - 1) return;
@@ -92,17 +92,17 @@ bool arrived(const Ctx& c, int mode, unsigned nslots, unsigned long long seq) {
 }
 
 template <int N>
-double run(Ctx& c, hipStream_t s, unsigned blocks, int mode, int iters, bool query0) {
+double run(Ctx& c, hipStream_t s, unsigned blocks, int mode, int iters, bool query0, unsigned gmin = 32) {
   Arg<N> a{};
   for (int i = 0; i < N / 4; i++) a.w[i] = i;
-  const unsigned gsz = std::max(32u, (blocks + kGroups - 1) / kGroups);  // as the kernel
+  const unsigned gsz = std::max(gmin, (blocks + kGroups - 1) / kGroups);  // as the kernel
   const unsigned nslots = (blocks + gsz - 1) / gsz;
   double t0 = 0;
   for (int it = -20; it < iters; it++) {
     if (it == 0) t0 = now_us();
     const unsigned long long seq = ++c.seq;
     if (query0 && hipStreamQuery(nullptr) != hipSuccess) c.misses += 1000000;  // the null stream is idle here
-    hipLaunchKernelGGL((probe<N>), dim3(blocks), dim3(256), 0, s, a, c.cnt, c.d_mail, seq, mode);
+    hipLaunchKernelGGL((probe<N>), dim3(blocks), dim3(256), 0, s, a, c.cnt, c.d_mail, seq, mode, gmin);
     if (mode != kSync) {
       const double start = now_us();
       while (!arrived(c, mode, nslots, seq)) {
@@ -153,6 +153,15 @@ int main(int argc, char** argv) {
                  kind == 2 ? "nonblocking+query0" : kind ? "nonblocking" : "blocking", blocks, names[mode], bytes, iters, us, c.misses);
           fflush(stdout);
         }
+  // tree group size sweep (the library uses max(32, n / 256)), blocking stream, 2 KiB
+  for (unsigned blocks : {256u, 1024u})
+    for (unsigned gmin : {4u, 8u, 16u, 32u, 64u}) {
+      const double us = run<2048>(c, sb, blocks, kTree, iters, false, gmin);
+      printf("{\"stream\": \"blocking\", \"blocks\": %u, \"completion\": \"tree\", \"group_min\": %u, "
+             "\"karg_bytes\": 2048, \"iters\": %d, \"us_per_call\": %.3f, \"mail_misses\": %lld}\n",
+             blocks, gmin, iters, us, c.misses);
+      fflush(stdout);
+    }
   (void)hipStreamDestroy(sb);
   (void)hipStreamDestroy(snb);
   (void)hipHostFree(h);
