@@ -6,16 +6,17 @@ clock, reduced to medians.
 
   python3 tools/dropin_timeline.py DIR KERNEL_SUBSTR [--skip N]
 
-Columns (medians over calls, microseconds):
-  call          launch start -> next call's launch start (the per-call period)
-  pre_launch    previous kernel launch's API end... i.e. host work before the
-                launch: end of the previous call's wait -> this launch start
-                (pointer queries, table lookup, argument packing)
-  launch_api    hipLaunchKernel duration
-  launch_to_start  hipLaunchKernel start -> kernel start on the device
-  kernel        kernel duration
-  end_to_next   kernel end -> next launch start (completion detection, the
-                return to the caller and the caller's loop)
+Fields (medians over calls, microseconds):
+  call_us                one launch start to the next (the per-call period)
+  launch_api_us          hipLaunchKernel duration
+  launch_to_start_us     hipLaunchKernel start -> kernel start on the device
+  kernel_us              kernel duration
+  end_to_next_launch_us  kernel end -> next launch start (completion
+                         detection, the return to the caller, the caller's
+                         loop; negative when the host sees the mailbox before
+                         the kernel's end timestamp)
+  other_api_us_per_call  every other HIP API call inside one call period, by
+                         name (median total per call)
 """
 import csv
 import statistics
