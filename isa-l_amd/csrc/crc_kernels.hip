@@ -174,8 +174,12 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t crc_mulmod(uint32_t 
 // VEC: 16-byte aligned shards (one dwordx4 per lane and tile); otherwise byte loads.
 // ---------------------------------------------------------------------------
 // Full tiles are read kCrcBatch at a time (all loads issued before any lookup):
-// one 16-byte load in flight per lane leaves the kernel latency-bound.
-constexpr unsigned kCrcBatch = 8;
+// one 16-byte load in flight per lane leaves the kernel latency-bound. Batches
+// of 4 (71 VGPRs, 7 waves per SIMD) beat 8 (111, 4) and 6 (93, 5) on the C2
+// shape: 0.7529 / 0.7576 -> 0.7620 / 0.7631 of 8 TB/s, two interleaved rounds
+// (profiles/r05/r05_crc_batch_ab.txt): the table lookups overlap the VALU
+// better with more waves.
+constexpr unsigned kCrcBatch = 4;
 
 // Shards that are not 16-byte aligned (byte loads, one Z^4096 chain step per
 // tile); aligned shards take crc32c_shards_pre below. (A chain step of four
