@@ -162,6 +162,61 @@ int main(int argc, char** argv) {
              blocks, gmin, iters, us, c.misses);
       fflush(stdout);
     }
+  // launch API: hipLaunchKernel (the <<<>>> path the library uses) vs
+  // hipModuleLaunchKernel with the argument block passed as one buffer
+  // (HIP_LAUNCH_PARAM_BUFFER_POINTER) on a function handle looked up once
+  {
+    hipFunction_t f = nullptr;
+    if (hipGetFuncBySymbol(&f, reinterpret_cast<const void*>(probe<2048>)) == hipSuccess && f) {
+      struct {
+        Arg<2048> a;
+        unsigned* cnt;
+        unsigned long long* mail;
+        unsigned long long seq;
+        int mode;
+        unsigned gmin;
+      } buf{};
+      for (int i = 0; i < 512; i++) buf.a.w[i] = i;
+      buf.cnt = c.cnt;
+      buf.mail = c.d_mail;
+      buf.mode = kTree;
+      buf.gmin = 32;
+      size_t sz = sizeof(buf);
+      for (unsigned blocks : {1u, 256u, 1024u}) {
+        double t0 = 0;
+        for (int it = -20; it < iters; it++) {
+          if (it == 0) t0 = now_us();
+          buf.seq = ++c.seq;
+          void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &buf, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                           HIP_LAUNCH_PARAM_END};
+          if (hipModuleLaunchKernel(f, blocks, 1, 1, 256, 1, 1, 0, sb, nullptr, extra) != hipSuccess) {
+            c.misses += 1000000;
+            break;
+          }
+          const double start = now_us();
+          while (c.h_mail[0] != buf.seq) {
+            if (now_us() - start > 100000.0) {
+              c.misses++;
+              break;
+            }
+          }
+          if ((it & 63) == 63) (void)hipStreamSynchronize(sb);
+        }
+        const double us = (now_us() - t0) / iters;
+        (void)hipStreamSynchronize(sb);
+        printf("{\"stream\": \"blocking\", \"blocks\": %u, \"completion\": \"tree\", \"launch\": "
+               "\"hipModuleLaunchKernel+buffer\", \"karg_bytes\": 2048, \"iters\": %d, \"us_per_call\": %.3f, "
+               "\"mail_misses\": %lld}\n",
+               blocks, iters, us, c.misses);
+        fflush(stdout);
+        printf("{\"stream\": \"blocking\", \"blocks\": %u, \"completion\": \"tree\", \"launch\": "
+               "\"hipLaunchKernel\", \"karg_bytes\": 2048, \"iters\": %d, \"us_per_call\": %.3f, "
+               "\"mail_misses\": %lld}\n",
+               blocks, iters, run<2048>(c, sb, blocks, kTree, iters, false, 32), c.misses);
+        fflush(stdout);
+      }
+    }
+  }
   (void)hipStreamDestroy(sb);
   (void)hipStreamDestroy(snb);
   (void)hipHostFree(h);
