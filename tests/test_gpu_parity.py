@@ -2017,6 +2017,47 @@ def test_raid_check_routes_vs_oracle(engine, oracle, gpu, monkeypatch, xor, karg
             assert got == oracle.raid(name, v, n, ref), (name, j, i, got)
 
 
+def test_raid6_batch_full_size_vs_oracle(engine, oracle, gpu):
+    """The bench's pq_gen / pq_check shape at full size (10 sources, 1 MiB x
+    1024 stripes, raid_base.c:44-140 coefficients: P all ones, Q = 2^j): every
+    P and Q byte == the oracle's (chunked), the batch check finds every stripe
+    consistent, then one flipped byte in a source / P / Q of three stripes is
+    reported at its column and the first mismatching row (a source byte
+    breaks P first), the rest stay consistent."""
+    import torch
+
+    k, rows, n, ns = 10, 2, 1 << 20, 1024
+    coef = np.ones(k * rows, np.uint8)
+    q = 1
+    for j in range(k):
+        coef[k + j] = q
+        q = engine.gf_mul(q, 2)
+    tbls = engine.ec_init_tables(k, rows, coef)
+    data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, 4242)
+    b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+    b.encode(0)
+    torch.cuda.synchronize()
+    _check_stripes_vs_oracle(oracle, coef, k, rows, lambda s: [data[s, j] for j in range(k)], coding, ns)
+    bad = torch.zeros(ns, dtype=torch.int64, device=gpu)
+    b.check(bad, 0)
+    torch.cuda.synchronize()
+    assert bool((bad == -1).all())
+    flips = {0: (3, 12345, 0), ns // 2: (k, n - 1, 0), ns - 1: (k + 1, 777777, 1)}  # stripe: (shard, col, row)
+    for s, (which, col, _) in flips.items():
+        t = data[s, which] if which < k else coding[s, which - k]
+        t[col] ^= 0x10
+    b.check(bad, 0)
+    torch.cuda.synchronize()
+    got = _host(bad)
+    for s in range(ns):
+        if s in flips:
+            _, col, row = flips[s]
+            assert int(got[s]) == (col << 8) | row, (s, hex(int(got[s])))
+        else:
+            assert got[s] == -1, s
+    b.close()
+
+
 @pytest.mark.parametrize("xor", ["1", "0"])
 @pytest.mark.parametrize("k,rows,n,ns", [
     (10, 2, 65536, 24),      # RAID-6 shape: XOR path, group 10
