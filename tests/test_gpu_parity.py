@@ -2037,7 +2037,8 @@ def test_raid6_batch_full_size_vs_oracle(engine, oracle, gpu):
     b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
     b.encode(0)
     torch.cuda.synchronize()
-    _check_stripes_vs_oracle(oracle, coef, k, rows, lambda s: [data[s, j] for j in range(k)], coding, ns)
+    _check_stripes_vs_oracle(oracle, coef, k, rows, lambda s: [data[s, j] for j in range(k)], coding, ns,
+                             chunk=16)
     bad = torch.zeros(ns, dtype=torch.int64, device=gpu)
     b.check(bad, 0)
     torch.cuda.synchronize()
