@@ -39,9 +39,12 @@ __global__ __launch_bounds__(kBlock) void copy_tiles(uint64_t dst, uint64_t src,
 // stores — the encode with its GF arithmetic replaced by one XOR fold. P = 0 is
 // a read-only pass (the check kernels' shape). Layout as bench.py allocates it:
 // data[S][K][len], coding[S][P][len].
-template <int K, int P>
+// PT: the shard addresses come from a device pointer table (per stripe: K
+// sources then P outputs), as the batch encode reads them, instead of being
+// computed from the layout.
+template <int K, int P, bool PT>
 __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t coding, int len, unsigned tiles,
-                                                     unsigned nitems) {
+                                                     unsigned nitems, const uint64_t* __restrict__ ptrs) {
   extern __shared__ unsigned lds_pad[];  // the encode's occupancy cap (dynamic LDS), unused
   const unsigned per = nitems / 8;
   const unsigned w = blockIdx.x;
@@ -53,7 +56,9 @@ __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t cod
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const auto r = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(data + (static_cast<uint64_t>(s) * K + j) * static_cast<uint64_t>(len)), 0, len,
+        reinterpret_cast<void*>(PT ? ptrs[static_cast<size_t>(s) * (K + P) + j]
+                                   : data + (static_cast<uint64_t>(s) * K + j) * static_cast<uint64_t>(len)),
+        0, len,
         0x00020000);
     v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2 /* nt */);
   }
@@ -67,8 +72,9 @@ __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t cod
 #pragma unroll
   for (int l = 0; l < P; ++l) {
     const auto r = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(coding + (static_cast<uint64_t>(s) * P + l) * static_cast<uint64_t>(len)), 0,
-        len, 0x00020000);
+        reinterpret_cast<void*>(PT ? ptrs[static_cast<size_t>(s) * (K + P) + K + l]
+                                   : coding + (static_cast<uint64_t>(s) * P + l) * static_cast<uint64_t>(len)),
+        0, len, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(acc ^ l, r, off, 0, 2 /* nt */);
   }
 }
@@ -79,23 +85,39 @@ __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t cod
 // two warm-ups with `lds` bytes of dynamic LDS per workgroup; returns the
 // rate in GB/s of (K + P) * len * S bytes per pass, or a negative error.
 extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p, unsigned stripes, int reps,
-                                 unsigned lds) {
+                                 unsigned lds, int use_ptrs) {
   if (len <= 0 || len % kTile || reps <= 0 || stripes == 0) return -1.0;
   const unsigned tiles = static_cast<unsigned>(len / kTile), nitems = tiles * stripes;
-  void (*kern)(uint64_t, uint64_t, int, unsigned, unsigned) = nullptr;
+  void (*kern)(uint64_t, uint64_t, int, unsigned, unsigned, const uint64_t*) = nullptr;
   switch (k * 100 + p) {
-    case 101: kern = skel_tiles<1, 1>; break;
-    case 1004: kern = skel_tiles<10, 4>; break;
-    case 1000: kern = skel_tiles<10, 0>; break;
-    case 1200: kern = skel_tiles<12, 0>; break;
-    case 1002: kern = skel_tiles<10, 2>; break;
-    case 1006: kern = skel_tiles<10, 6>; break;
-    case 1008: kern = skel_tiles<10, 8>; break;
-    case 2006: kern = skel_tiles<20, 6>; break;
-    case 2008: kern = skel_tiles<20, 8>; break;
-    case 1003: kern = skel_tiles<10, 3>; break;
-    case 706: kern = skel_tiles<7, 6>; break;  // C4 update: 1 source + 6 parity read, 6 parity written
+    case 101: kern = use_ptrs ? skel_tiles<1, 1, true> : skel_tiles<1, 1, false>; break;
+    case 1004: kern = use_ptrs ? skel_tiles<10, 4, true> : skel_tiles<10, 4, false>; break;
+    case 1000: kern = use_ptrs ? skel_tiles<10, 0, true> : skel_tiles<10, 0, false>; break;
+    case 1200: kern = use_ptrs ? skel_tiles<12, 0, true> : skel_tiles<12, 0, false>; break;
+    case 1002: kern = use_ptrs ? skel_tiles<10, 2, true> : skel_tiles<10, 2, false>; break;
+    case 1001: kern = use_ptrs ? skel_tiles<10, 1, true> : skel_tiles<10, 1, false>; break;
+    case 1006: kern = use_ptrs ? skel_tiles<10, 6, true> : skel_tiles<10, 6, false>; break;
+    case 1008: kern = use_ptrs ? skel_tiles<10, 8, true> : skel_tiles<10, 8, false>; break;
+    case 2006: kern = use_ptrs ? skel_tiles<20, 6, true> : skel_tiles<20, 6, false>; break;
+    case 2008: kern = use_ptrs ? skel_tiles<20, 8, true> : skel_tiles<20, 8, false>; break;
+    case 1003: kern = use_ptrs ? skel_tiles<10, 3, true> : skel_tiles<10, 3, false>; break;
+    case 706: kern = use_ptrs ? skel_tiles<7, 6, true> : skel_tiles<7, 6, false>; break;  // C4 update: 1 source + 6 parity read, 6 parity written
     default: return -4.0;
+  }
+  uint64_t* d_ptrs = nullptr;
+  if (use_ptrs) {
+    const size_t np = static_cast<size_t>(stripes) * (k + p);
+    uint64_t* h = static_cast<uint64_t*>(malloc(np * 8));
+    if (!h) return -5.0;
+    for (unsigned st = 0; st < stripes; ++st) {
+      for (int j = 0; j < k; ++j)
+        h[st * (k + p) + j] = reinterpret_cast<uint64_t>(data) + (static_cast<uint64_t>(st) * k + j) * len;
+      for (int l = 0; l < p; ++l)
+        h[st * (k + p) + k + l] = reinterpret_cast<uint64_t>(coding) + (static_cast<uint64_t>(st) * p + l) * len;
+    }
+    const bool ok = hipMalloc(&d_ptrs, np * 8) == hipSuccess && hipMemcpy(d_ptrs, h, np * 8, hipMemcpyHostToDevice) == hipSuccess;
+    free(h);
+    if (!ok) return -5.0;
   }
   hipStream_t st;
   hipEvent_t e0, e1;
@@ -105,7 +127,7 @@ extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p
   for (int i = 0; i < reps + 2; ++i) {
     if (i == 2) (void)hipEventRecord(e0, st);
     hipLaunchKernelGGL(kern, dim3(nitems), dim3(kBlock), lds, st, reinterpret_cast<uint64_t>(data),
-                       reinterpret_cast<uint64_t>(coding), len, tiles, nitems);
+                       reinterpret_cast<uint64_t>(coding), len, tiles, nitems, d_ptrs);
   }
   (void)hipEventRecord(e1, st);
   const hipError_t err = hipEventSynchronize(e1);
@@ -114,6 +136,7 @@ extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipStreamDestroy(st);
+  if (d_ptrs) (void)hipFree(d_ptrs);
   if (err != hipSuccess || ms <= 0.f) return -3.0;
   return static_cast<double>(k + p) * len * stripes * reps / (ms * 1e-3) / 1e9;
 }

@@ -5,7 +5,8 @@ source shards and writes P output shards per stripe exactly as the encode
 does (16 B per lane, 4 KiB column tiles, XCD-contiguous items, nt buffer
 loads/stores) with the GF arithmetic replaced by one XOR fold. Prints one JSON
 line per (shape, LDS cap): GB/s of (K+P)*len*S per pass and the fraction of
-8 TB/s. Run on the GPU box: python3 tools/skel_probe.py [REPS]
+8 TB/s. `pointer_table`: the shard addresses are read from a device pointer
+table as the batch encode does, instead of computed from the layout. Run on the GPU box: python3 tools/skel_probe.py [REPS]
 """
 import ctypes
 import json
@@ -21,6 +22,7 @@ SHAPES = [  # (label, k, p, len, stripes)
     ("C2 encode k10p4", 10, 4, MiB, 1024),
     ("C3 decode k10 -> 3", 10, 3, MiB, 1024),
     ("pq_gen k10p2", 10, 2, MiB, 1024),
+    ("xor_gen k10p1", 10, 1, MiB, 1024),
     ("k10p6", 10, 6, MiB, 1024),
     ("k10p8", 10, 8, MiB, 1024),
     ("k20p6", 20, 6, 4 * MiB, 64),
@@ -33,19 +35,23 @@ SHAPES = [  # (label, k, p, len, stripes)
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    only = sys.argv[2] if len(sys.argv) > 2 else None  # shape-label substring
     lib = ctypes.CDLL(os.path.join(REPO, "tools", "libcopy_probe.so"))
     lib.skel_probe_gbs.restype = ctypes.c_double
     lib.skel_probe_gbs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                   ctypes.c_uint, ctypes.c_int, ctypes.c_uint]
+                                   ctypes.c_uint, ctypes.c_int, ctypes.c_uint, ctypes.c_int]
     data = torch.empty(12 << 30, dtype=torch.uint8, device="cuda")
     data.view(torch.int32).random_()
     coding = torch.empty(8 << 30, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     for label, k, p, n, s in SHAPES:
+        if only and only not in label:
+            continue
         assert k * n * s <= data.numel() and p * n * s <= coding.numel()
-        for lds in (0, 32768):
-            g = lib.skel_probe_gbs(data.data_ptr(), coding.data_ptr(), n, k, p, s, reps, lds)
+        for lds, ptrs in ((0, 0), (32768, 0), (32768, 1)):
+            g = lib.skel_probe_gbs(data.data_ptr(), coding.data_ptr(), n, k, p, s, reps, lds, ptrs)
             print(json.dumps({"shape": label, "k": k, "p": p, "len": n, "stripes": s, "lds_bytes": lds,
+                              "pointer_table": bool(ptrs),
                               "reps": reps, "gb_s": round(g, 1), "frac_of_8tbs": round(g / 8000.0, 4)}),
                   flush=True)
 
