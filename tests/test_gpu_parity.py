@@ -8,6 +8,7 @@ oracle spot checks of sampled stripes).
 """
 import os
 import subprocess
+import sys
 import threading
 
 import numpy as np
@@ -506,6 +507,28 @@ def test_dropin_kernel_args_vs_oracle(engine, oracle, gpu, monkeypatch, capfd, n
         base = (k + l) * stride
         assert np.array_equal(out[base: base + n], want[l]), l
         assert np.array_equal(out[base + n: base + stride], canary[l * stride + n: (l + 1) * stride]), l
+
+
+def test_device_resident_failure_aborts_naming_the_call(gpu):
+    """DESIGN §2 'Failures': a call with device-resident shards cannot fall back
+    to the CPU route, so a failing HIP step aborts the process with the step
+    named. A child process makes one kernel-argument call with a fault
+    injected at the allocation site (ISAL_HIP_FAULT=1: before any launch, so
+    no GPU work is in flight when it aborts)."""
+    code = (
+        "import sys; sys.path.insert(0, 'isa-l_amd'); import torch, isal_amd as e\n"
+        "k, r, n = 4, 2, 65536\n"
+        "a = e.gf_gen_rs_matrix(k + r, k); t = e.ec_init_tables(k, r, a[k * k:])\n"
+        "b = torch.zeros((k + r, n), dtype=torch.uint8, device='cuda')\n"
+        "e.ec_encode_data(n, k, r, t, [b[j] for j in range(k)], [b[k + l] for l in range(r)])\n"
+        "print('returned')\n")
+    env = {x: v for x, v in os.environ.items() if not x.startswith("ISAL_HIP_")}
+    env["ISAL_HIP_FAULT"] = "1"
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=ecutil.REPO,
+                       timeout=300)
+    assert p.returncode != 0 and "returned" not in p.stdout, (p.returncode, p.stdout, p.stderr[-2000:])
+    assert "ensure_done" in p.stderr and "device-resident shards" in p.stderr and "aborting" in p.stderr, \
+        p.stderr[-2000:]
 
 
 def test_dropin_lane_width_follows_concurrency(gpu):
