@@ -39,6 +39,25 @@ def gpu():
     return torch.device("cuda:0")
 
 
+def pytest_runtest_teardown(item):
+    """ISAL_TEST_RSS_LOG=<file>: append each test's id, the process's peak RSS
+    after it and the current RSS split (anonymous / file-backed / shmem, MiB),
+    to find the test that sets the suite's peak and what kind of pages it is."""
+    path = os.environ.get("ISAL_TEST_RSS_LOG")
+    if path:
+        import resource
+
+        cur = {}
+        with open("/proc/self/status") as st:
+            for line in st:
+                if line.startswith(("RssAnon", "RssFile", "RssShmem")):
+                    key, val = line.split(":")
+                    cur[key] = int(val.split()[0]) // 1024
+        with open(path, "a") as f:
+            f.write(f"{item.nodeid} {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024} "
+                    + " ".join(f"{k_}={v}" for k_, v in cur.items()) + "\n")
+
+
 def pytest_terminal_summary(terminalreporter):
     """Peak resident memory of the test process (the GPU tier's full-size
     C2/C3/C4 host arrays are freed after each test; DESIGN §5 records it)."""

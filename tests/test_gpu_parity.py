@@ -562,38 +562,52 @@ def test_config_c1_cauchy_k4_p2_64k(engine, gpu):
     assert [ecutil.oracle().fnv(d) for d in dst] == case["fnv"]
 
 
-def _oracle_encode_all(oracle, coef, k, rows, srcs, threads=16):
-    """Oracle parity of many stripes at once: srcs[s] = list of k host arrays.
-    ctypes releases the GIL inside the oracle, so the stripes run in parallel
-    on the host cores (the oracle is the checker, never the code under test)."""
+def _oracle_encode_all(oracle, coef, k, rows, srcs, threads=16, out=None):
+    """Oracle parity of many stripes at once: srcs[s] = list of k host arrays;
+    returns (or fills) out[s, row]. ctypes releases the GIL inside the oracle,
+    so the stripes run in parallel on the host cores (the oracle is the
+    checker, never the code under test). The outputs are one block allocated
+    here, not per worker thread: 1 MiB arrays allocated in worker threads and
+    freed in this one stayed resident in glibc's per-thread arenas (the GPU
+    suite's peak RSS reached 12 GiB, profiles/r05/r05_rss_probe.txt)."""
     from concurrent.futures import ThreadPoolExecutor
 
     tbls = oracle.ec_init_tables(k, rows, coef)
     n = len(srcs[0][0])
+    if out is None:
+        out = np.empty((len(srcs), rows, n), np.uint8)
 
-    def one(src):
-        dst = [np.zeros(n, np.uint8) for _ in range(rows)]
-        oracle.ec_encode_data(n, k, rows, tbls, src, dst)
-        return dst
+    def one(i):
+        oracle.ec_encode_data(n, k, rows, tbls, srcs[i], [out[i, l] for l in range(rows)])
 
     with ThreadPoolExecutor(max_workers=min(threads, os.cpu_count() or 1)) as ex:
-        return list(ex.map(one, srcs))
+        list(ex.map(one, range(len(srcs))))
+    return out
 
 
 def _check_stripes_vs_oracle(oracle, coef, k, rows, srcs_of, out, ns, chunk=64):
     """out[s] (device, rows x n) == the oracle's encode of srcs_of(s) (a list
-    of k device shards) for every stripe s, `chunk` stripes at a time so the
-    host holds ~chunk x (k + rows) shards, not the whole batch (the full-size
-    C2/C3 tests used to keep ~20 GiB of host arrays alive)."""
+    of k device shards) for every stripe s, `chunk` stripes at a time through
+    three host blocks allocated once (sources, oracle parity, device parity),
+    so the host holds ~chunk x (k + 2 rows) shards, not the whole batch."""
+    import torch
+
+    n = int(out.shape[-1])
+    c = min(chunk, ns)
+    src = np.empty((c, k, n), np.uint8)
+    want = np.empty((c, rows, n), np.uint8)
+    got = np.empty((c, rows, n), np.uint8)
     for s0 in range(0, ns, chunk):
         s1 = min(ns, s0 + chunk)
-        srcs = [[_host(x) for x in srcs_of(s)] for s in range(s0, s1)]
-        want = _oracle_encode_all(oracle, coef, k, rows, srcs)
-        got = _host(out[s0:s1])
+        for i, s in enumerate(range(s0, s1)):
+            for j, x in enumerate(srcs_of(s)):
+                torch.from_numpy(src[i, j]).copy_(x)
+        torch.from_numpy(got[:s1 - s0]).copy_(out[s0:s1])
+        _oracle_encode_all(oracle, coef, k, rows, [[src[i, j] for j in range(k)] for i in range(s1 - s0)],
+                           out=want)
         for i in range(s1 - s0):
             for l in range(rows):
-                assert np.array_equal(got[i, l], want[i][l]), (s0 + i, l)
-        del srcs, want, got
+                assert np.array_equal(got[i, l], want[i, l]), (s0 + i, l)
 
 
 def test_config_c2_c3_full_size(engine, oracle, gpu):
@@ -1189,7 +1203,7 @@ def test_fused_crc_derived_xor_rows(engine, oracle, gpu, monkeypatch, xrows, k, 
     g64 = [int(v) & 0xFFFFFFFFFFFFFFFF for v in c64.tolist()]
     assert np.array_equal(_host(coding), hc)
     for s in range(ns):
-        shards = [h[s, j] for j in range(k)] + want[s]
+        shards = [h[s, j] for j in range(k)] + list(want[s])
         for l in range(rows):
             assert np.array_equal(hc[s, l], want[s][l]), (s, l)
         for i, buf in enumerate(shards):
