@@ -42,15 +42,19 @@ __global__ __launch_bounds__(kBlock) void copy_tiles(uint64_t dst, uint64_t src,
 // PT: the shard addresses come from a device pointer table (per stripe: K
 // sources then P outputs), as the batch encode reads them, instead of being
 // computed from the layout.
-template <int K, int P, bool PT>
+// T: consecutive 4 KiB tiles per workgroup (items = stripes x tiles / T), one
+// after the other with the item's address arithmetic shared.
+template <int K, int P, bool PT, int T = 1>
 __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t coding, int len, unsigned tiles,
                                                      unsigned nitems, const uint64_t* __restrict__ ptrs) {
   extern __shared__ unsigned lds_pad[];  // the encode's occupancy cap (dynamic LDS), unused
   const unsigned per = nitems / 8;
   const unsigned w = blockIdx.x;
   const unsigned item = (nitems % 8) ? w : (w % 8) * per + w / 8;
-  const unsigned s = item / tiles, t = item % tiles;
-  const int off = static_cast<int>(t) * kTile + threadIdx.x * 16;
+  const unsigned s = item / (tiles / T), t = (item % (tiles / T)) * T;
+#pragma unroll
+  for (int h = 0; h < T; ++h) {
+  const int off = static_cast<int>(t + h) * kTile + threadIdx.x * 16;
   typedef int v4i __attribute__((ext_vector_type(4)));
   v4i v[K];
 #pragma unroll
@@ -67,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t cod
   for (int j = 1; j < K; ++j) acc ^= v[j];
   if (P == 0) {
     if (acc.x == 0x7eadbeef && acc.y == 0x1234567 && acc.z == 0x89abcdef && acc.w == 0x0f1e2d3c) lds_pad[0] = 1;
-    return;
+    continue;
   }
 #pragma unroll
   for (int l = 0; l < P; ++l) {
@@ -77,6 +81,7 @@ __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t cod
         0, len, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(acc ^ l, r, off, 0, 2 /* nt */);
   }
+  }
 }
 
 }  // namespace
@@ -84,12 +89,22 @@ __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t cod
 // Runs the (K, P) skeleton over S stripes of len-byte shards `reps` times after
 // two warm-ups with `lds` bytes of dynamic LDS per workgroup; returns the
 // rate in GB/s of (K + P) * len * S bytes per pass, or a negative error.
+// use_ptrs: bit 0 the pointer table; bits 8+ T, tiles per workgroup (1, 2 or
+// 4; the xor_gen / pq_gen / C2 shapes only for T > 1).
 extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p, unsigned stripes, int reps,
                                  unsigned lds, int use_ptrs) {
-  if (len <= 0 || len % kTile || reps <= 0 || stripes == 0) return -1.0;
-  const unsigned tiles = static_cast<unsigned>(len / kTile), nitems = tiles * stripes;
+  const int tpi = (use_ptrs >> 8) ? (use_ptrs >> 8) : 1;
+  use_ptrs &= 1;
+  if (len <= 0 || len % (kTile * tpi) || reps <= 0 || stripes == 0) return -1.0;
+  const unsigned tiles = static_cast<unsigned>(len / kTile), nitems = tiles * stripes / tpi;
   void (*kern)(uint64_t, uint64_t, int, unsigned, unsigned, const uint64_t*) = nullptr;
-  switch (k * 100 + p) {
+  switch (k * 100 + p + 100000 * (tpi - 1)) {
+    case 101001: kern = use_ptrs ? skel_tiles<10, 1, true, 2> : skel_tiles<10, 1, false, 2>; break;
+    case 101002: kern = use_ptrs ? skel_tiles<10, 2, true, 2> : skel_tiles<10, 2, false, 2>; break;
+    case 101004: kern = use_ptrs ? skel_tiles<10, 4, true, 2> : skel_tiles<10, 4, false, 2>; break;
+    case 301001: kern = use_ptrs ? skel_tiles<10, 1, true, 4> : skel_tiles<10, 1, false, 4>; break;
+    case 301002: kern = use_ptrs ? skel_tiles<10, 2, true, 4> : skel_tiles<10, 2, false, 4>; break;
+    case 301004: kern = use_ptrs ? skel_tiles<10, 4, true, 4> : skel_tiles<10, 4, false, 4>; break;
     case 101: kern = use_ptrs ? skel_tiles<1, 1, true> : skel_tiles<1, 1, false>; break;
     case 1004: kern = use_ptrs ? skel_tiles<10, 4, true> : skel_tiles<10, 4, false>; break;
     case 1000: kern = use_ptrs ? skel_tiles<10, 0, true> : skel_tiles<10, 0, false>; break;

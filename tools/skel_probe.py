@@ -6,7 +6,10 @@ does (16 B per lane, 4 KiB column tiles, XCD-contiguous items, nt buffer
 loads/stores) with the GF arithmetic replaced by one XOR fold. Prints one JSON
 line per (shape, LDS cap): GB/s of (K+P)*len*S per pass and the fraction of
 8 TB/s. `pointer_table`: the shard addresses are read from a device pointer
-table as the batch encode does, instead of computed from the layout. Run on the GPU box: python3 tools/skel_probe.py [REPS]
+table as the batch encode does, instead of computed from the layout.
+`tiles_per_wg` (TILES=1,2,4 in the environment; the xor_gen / pq_gen / C2
+shapes only above 1): consecutive 4 KiB tiles per workgroup.
+Run on the GPU box: python3 tools/skel_probe.py [REPS [SHAPE]]
 """
 import ctypes
 import json
@@ -48,10 +51,11 @@ def main():
         if only and only not in label:
             continue
         assert k * n * s <= data.numel() and p * n * s <= coding.numel()
-        for lds, ptrs in ((0, 0), (32768, 0), (32768, 1)):
-            g = lib.skel_probe_gbs(data.data_ptr(), coding.data_ptr(), n, k, p, s, reps, lds, ptrs)
+        for tpi in [int(t) for t in os.environ.get("TILES", "1").split(",")]:
+          for lds, ptrs in ((0, 0), (32768, 0), (32768, 1)):
+            g = lib.skel_probe_gbs(data.data_ptr(), coding.data_ptr(), n, k, p, s, reps, lds, ptrs | (tpi << 8))
             print(json.dumps({"shape": label, "k": k, "p": p, "len": n, "stripes": s, "lds_bytes": lds,
-                              "pointer_table": bool(ptrs),
+                              "pointer_table": bool(ptrs), "tiles_per_wg": tpi,
                               "reps": reps, "gb_s": round(g, 1), "frac_of_8tbs": round(g / 8000.0, 4)}),
                   flush=True)
 
