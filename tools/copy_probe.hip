@@ -44,8 +44,9 @@ __global__ __launch_bounds__(kBlock) void copy_tiles(uint64_t dst, uint64_t src,
 // computed from the layout.
 // T: consecutive 4 KiB tiles per workgroup (items = stripes x tiles / T), one
 // after the other with the item's address arithmetic shared.
-template <int K, int P, bool PT, int T = 1>
-__global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t coding, int len, unsigned tiles,
+// B: threads per workgroup (a tile is B x 16 bytes; the encode's 256 by default).
+template <int K, int P, bool PT, int T = 1, int B = kBlock>
+__global__ __launch_bounds__(B) void skel_tiles(uint64_t data, uint64_t coding, int len, unsigned tiles,
                                                      unsigned nitems, const uint64_t* __restrict__ ptrs) {
   extern __shared__ unsigned lds_pad[];  // the encode's occupancy cap (dynamic LDS), unused
   const unsigned per = nitems / 8;
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t cod
   const unsigned s = item / (tiles / T), t = (item % (tiles / T)) * T;
 #pragma unroll
   for (int h = 0; h < T; ++h) {
-  const int off = static_cast<int>(t + h) * kTile + threadIdx.x * 16;
+  const int off = static_cast<int>(t + h) * (B * 16) + threadIdx.x * 16;
   typedef int v4i __attribute__((ext_vector_type(4)));
   v4i v[K];
 #pragma unroll
@@ -89,16 +90,24 @@ __global__ __launch_bounds__(kBlock) void skel_tiles(uint64_t data, uint64_t cod
 // Runs the (K, P) skeleton over S stripes of len-byte shards `reps` times after
 // two warm-ups with `lds` bytes of dynamic LDS per workgroup; returns the
 // rate in GB/s of (K + P) * len * S bytes per pass, or a negative error.
-// use_ptrs: bit 0 the pointer table; bits 8+ T, tiles per workgroup (1, 2 or
-// 4; the xor_gen / pq_gen / C2 shapes only for T > 1).
+// use_ptrs: bit 0 the pointer table; bits 8-15 T, tiles per workgroup (1, 2
+// or 4; the xor_gen / pq_gen / C2 shapes only for T > 1); bits 16+ threads per
+// workgroup other than 256 (128, 512 or 1024; xor_gen and C2 only, T = 1).
 extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p, unsigned stripes, int reps,
                                  unsigned lds, int use_ptrs) {
-  const int tpi = (use_ptrs >> 8) ? (use_ptrs >> 8) : 1;
+  const int tpi = ((use_ptrs >> 8) & 255) ? ((use_ptrs >> 8) & 255) : 1;
+  const int blk = (use_ptrs >> 16) ? (use_ptrs >> 16) : kBlock;
   use_ptrs &= 1;
-  if (len <= 0 || len % (kTile * tpi) || reps <= 0 || stripes == 0) return -1.0;
-  const unsigned tiles = static_cast<unsigned>(len / kTile), nitems = tiles * stripes / tpi;
+  if (len <= 0 || len % (blk * 16 * tpi) || reps <= 0 || stripes == 0) return -1.0;
+  const unsigned tiles = static_cast<unsigned>(len / (blk * 16)), nitems = tiles * stripes / tpi;
   void (*kern)(uint64_t, uint64_t, int, unsigned, unsigned, const uint64_t*) = nullptr;
-  switch (k * 100 + p + 100000 * (tpi - 1)) {
+  switch (k * 100 + p + 100000 * (tpi - 1) + 1000000 * (blk == kBlock ? 0 : blk)) {
+    case 128001001: kern = use_ptrs ? skel_tiles<10, 1, true, 1, 128> : skel_tiles<10, 1, false, 1, 128>; break;
+    case 512001001: kern = use_ptrs ? skel_tiles<10, 1, true, 1, 512> : skel_tiles<10, 1, false, 1, 512>; break;
+    case 1024001001: kern = use_ptrs ? skel_tiles<10, 1, true, 1, 1024> : skel_tiles<10, 1, false, 1, 1024>; break;
+    case 128001004: kern = use_ptrs ? skel_tiles<10, 4, true, 1, 128> : skel_tiles<10, 4, false, 1, 128>; break;
+    case 512001004: kern = use_ptrs ? skel_tiles<10, 4, true, 1, 512> : skel_tiles<10, 4, false, 1, 512>; break;
+    case 1024001004: kern = use_ptrs ? skel_tiles<10, 4, true, 1, 1024> : skel_tiles<10, 4, false, 1, 1024>; break;
     case 101001: kern = use_ptrs ? skel_tiles<10, 1, true, 2> : skel_tiles<10, 1, false, 2>; break;
     case 101002: kern = use_ptrs ? skel_tiles<10, 2, true, 2> : skel_tiles<10, 2, false, 2>; break;
     case 101004: kern = use_ptrs ? skel_tiles<10, 4, true, 2> : skel_tiles<10, 4, false, 2>; break;
@@ -141,7 +150,7 @@ extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p
   (void)hipEventCreate(&e1);
   for (int i = 0; i < reps + 2; ++i) {
     if (i == 2) (void)hipEventRecord(e0, st);
-    hipLaunchKernelGGL(kern, dim3(nitems), dim3(kBlock), lds, st, reinterpret_cast<uint64_t>(data),
+    hipLaunchKernelGGL(kern, dim3(nitems), dim3(blk), lds, st, reinterpret_cast<uint64_t>(data),
                        reinterpret_cast<uint64_t>(coding), len, tiles, nitems, d_ptrs);
   }
   (void)hipEventRecord(e1, st);

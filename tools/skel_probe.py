@@ -8,7 +8,9 @@ line per (shape, LDS cap): GB/s of (K+P)*len*S per pass and the fraction of
 8 TB/s. `pointer_table`: the shard addresses are read from a device pointer
 table as the batch encode does, instead of computed from the layout.
 `tiles_per_wg` (TILES=1,2,4 in the environment; the xor_gen / pq_gen / C2
-shapes only above 1): consecutive 4 KiB tiles per workgroup.
+shapes only above 1): consecutive 4 KiB tiles per workgroup. `threads_per_wg`
+(BLOCKS=256,128,512,1024; xor_gen and C2 only besides 256): a tile is
+threads x 16 bytes.
 Run on the GPU box: python3 tools/skel_probe.py [REPS [SHAPE]]
 """
 import ctypes
@@ -51,11 +53,13 @@ def main():
         if only and only not in label:
             continue
         assert k * n * s <= data.numel() and p * n * s <= coding.numel()
-        for tpi in [int(t) for t in os.environ.get("TILES", "1").split(",")]:
+        for blk in [int(b) for b in os.environ.get("BLOCKS", "256").split(",")]:
+         for tpi in [int(t) for t in os.environ.get("TILES", "1").split(",")]:
           for lds, ptrs in ((0, 0), (32768, 0), (32768, 1)):
-            g = lib.skel_probe_gbs(data.data_ptr(), coding.data_ptr(), n, k, p, s, reps, lds, ptrs | (tpi << 8))
+            code = ptrs | (tpi << 8) | ((blk if blk != 256 else 0) << 16)
+            g = lib.skel_probe_gbs(data.data_ptr(), coding.data_ptr(), n, k, p, s, reps, lds, code)
             print(json.dumps({"shape": label, "k": k, "p": p, "len": n, "stripes": s, "lds_bytes": lds,
-                              "pointer_table": bool(ptrs), "tiles_per_wg": tpi,
+                              "pointer_table": bool(ptrs), "tiles_per_wg": tpi, "threads_per_wg": blk,
                               "reps": reps, "gb_s": round(g, 1), "frac_of_8tbs": round(g / 8000.0, 4)}),
                   flush=True)
 
