@@ -176,20 +176,26 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_bytes(const uint64_t* __r
 // tables: a lane keeps b = Z^4080_u(a) in the u-domain, XORs it into the next
 // chunk's first 8 bytes like a CRC register and maps the chunk once, b' =
 // F'_u(chunk ^ b) — 28 lookups per tile and no chain step — the item's last
-// tile applies F_u and leaves the plain chain. Loads are double-buffered (the
-// next B tiles in flight). (A form with the lookups software-pipelined,
+// tile applies F_u and leaves the plain chain. (A form with the lookups software-pipelined,
 // ISAL_HIP_CRC64_PRE_PIPE=1, ran 2.94-2.95 vs 2.82-2.85 ms on C2 — 56 lookup
 // VGPRs in flight cut the occupancy from 7 to 3 waves per SIMD —
 // profiles/r03/r03_crc64_prepipe_benches.jsonl; removed in round 5, as was a
 // batch of 8 tiles, ISAL_HIP_CRC64_BATCH=8, measured slower.)
-constexpr int kPreBatch = 4;
+// Round 5: each workgroup runs TWO items, their chains interleaved step by
+// step, so a lane has two independent lookup chains in flight; B = 4 tiles of
+// each item are loaded together (72 VGPRs, 7 waves per SIMD). Same box, two
+// interleaved rounds, C2-shaped CRC64 (profiles/r05/r05_crc64_chains_ab.txt):
+// one chain with double-buffered loads 0.6542 / 0.6554 of 8 TB/s, two chains
+// 0.6671 / 0.6674; 3 or 4 chains, or 2 tiles per batch, measured between or
+// below (0.650-0.668).
+constexpr int kPreItems = 2, kPreBatch = 4;
 
 __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __restrict__ ptrs, int ptr_stride,
                                                            int nsh, int len, unsigned nitems, unsigned nblk,
                                                            unsigned tt, unsigned nfull, int uswap,
                                                            const uint64_t* __restrict__ tabs,
                                                            uint64_t* __restrict__ part) {
-  constexpr int B = kPreBatch;
+  constexpr int NI = kPreItems, B = kPreBatch;
   __shared__ uint64_t lt[2 * kCE];  // F_u, F'_u
   load_lds<2 * kCE>(lt, tabs + ISAL_HIP_CRC64_PRE_TAB);
   __syncthreads();
@@ -202,34 +208,48 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
       chunk_acc(c, lt + kCE, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
     return c;
   };
-  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
-    const unsigned si = w / nblk, blk = w - si * nblk;
-    const unsigned stripe = si / nsh, i = si - stripe * nsh;
-    const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
-    const unsigned t0 = blk * tt, t1 = t0 + tt < nfull ? t0 + tt : nfull;
-    X64 b{0u, 0u};
-    unsigned t = t0;
-    uint4 xn[B];
-    if (t + B <= t1) {
+  for (unsigned v = blockIdx.x; NI * v < nitems; v += gridDim.x) {
+    uint64_t base[NI];
+    unsigned t0[NI], t1[NI], n = ~0u;
+    X64 bc[NI];
 #pragma unroll
-      for (int g = 0; g < B; ++g) xn[g] = load16<kBufNT>(base, static_cast<long long>(t + g) * kTile + lane, len);
-    }
-    for (; t + B <= t1; t += B) {
-      uint4 x[B];
-#pragma unroll
-      for (int g = 0; g < B; ++g) x[g] = xn[g];
-      if (t + 2 * B <= t1) {
-#pragma unroll
-        for (int g = 0; g < B; ++g)
-          xn[g] = load16<kBufNT>(base, static_cast<long long>(t + B + g) * kTile + lane, len);
+    for (int q = 0; q < NI; ++q) {
+      const unsigned w = NI * v + q;
+      base[q] = 0;
+      t0[q] = t1[q] = 0;
+      if (w < nitems) {
+        const unsigned si = w / nblk, blk = w - si * nblk;
+        const unsigned stripe = si / nsh, i = si - stripe * nsh;
+        base[q] = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
+        t0[q] = blk * tt;
+        t1[q] = t0[q] + tt < nfull ? t0[q] + tt : nfull;
       }
-#pragma unroll
-      for (int g = 0; g < B; ++g) b = step(t + g, t1, b, x[g]);
+      n = min(n, t1[q] - t0[q]);
+      bc[q] = X64{0u, 0u};
     }
-    for (; t < t1; ++t)
-      b = step(t, t1, b, load16<kBufNT>(base, static_cast<long long>(t) * kTile + lane, len));
-    const uint64_t a = b.get();
-    part[static_cast<size_t>(w) * kBlock + threadIdx.x] = uswap ? __builtin_bswap64(a) : a;
+    unsigned i = 0;
+    for (; i + B <= n; i += B) {
+      uint4 x[NI][B];
+#pragma unroll
+      for (int g = 0; g < B; ++g)
+#pragma unroll
+        for (int q = 0; q < NI; ++q)
+          x[q][g] = load16<kBufNT>(base[q], static_cast<long long>(t0[q] + i + g) * kTile + lane, len);
+#pragma unroll
+      for (int g = 0; g < B; ++g)
+#pragma unroll
+        for (int q = 0; q < NI; ++q) bc[q] = step(t0[q] + i + g, t1[q], bc[q], x[q][g]);
+    }
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      for (unsigned j = t0[q] + i; j < t1[q]; ++j)
+        bc[q] = step(j, t1[q], bc[q], load16<kBufNT>(base[q], static_cast<long long>(j) * kTile + lane, len));
+      const unsigned w = NI * v + q;
+      if (w < nitems) {
+        const uint64_t r = bc[q].get();
+        part[static_cast<size_t>(w) * kBlock + threadIdx.x] = uswap ? __builtin_bswap64(r) : r;
+      }
+    }
   }
 }
 
@@ -765,8 +785,8 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
     if (g.nblk) {
       const unsigned nitems = static_cast<unsigned>(ns * nsh * g.nblk);
       if (vec16)
-        hipLaunchKernelGGL(crc64_shards_pre, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, nitems,
-                           static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
+        hipLaunchKernelGGL(crc64_shards_pre, dim3((nitems + kPreItems - 1) / kPreItems), dim3(kBlock), 0, s, ptrs,
+                           ptr_stride, nsh, len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
                            static_cast<unsigned>(g.nfull), !refl, d_tabs, part);
       else
         hipLaunchKernelGGL(crc64_shards_bytes, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, nitems,
