@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r05m; mkdir -p $O
+O=gpurun_out/${OUT:-r05m}; mkdir -p $O
 B="python3 bench.py"
 timeout -k 10 600 $B > $O/bench_c2.json 2> $O/bench_c2.err || { echo FAIL c2; tail $O/bench_c2.err; exit 1; }
 cat $O/bench_c2.json
