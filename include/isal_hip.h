@@ -26,6 +26,7 @@ extern "C" {
 #define ISAL_HIP_EINVAL (-1)   /* bad argument (size, count, NULL, unaligned pointer) */
 #define ISAL_HIP_EHIP (-2)     /* a HIP runtime call failed */
 #define ISAL_HIP_ENOMEM (-3)   /* host or device allocation failed */
+#define ISAL_HIP_EDEVICE (-4)  /* a shard pointer is on another GPU than the object's device */
 
 typedef struct isal_hip_batch isal_hip_batch;
 
@@ -37,6 +38,12 @@ typedef struct isal_hip_batch isal_hip_batch;
  * coding: host array of nstripes*rows DEVICE pointers (coding[s*rows + l]).
  * Pointer tables and derived coefficient tables are uploaded once here; the
  * launch functions below only enqueue kernels.
+ * The batch belongs to the caller's current device at creation: every shard
+ * must be hipMalloc memory of that device, managed memory, or page-locked host
+ * memory (ISAL_HIP_EDEVICE for memory of another GPU, ISAL_HIP_EINVAL for
+ * pageable memory, which no kernel can reach). The batch's kernels run on its
+ * device whatever the calling thread's current device is; a stream passed to
+ * them must belong to that device (NULL: its legacy default stream).
  */
 int isal_hip_batch_create(isal_hip_batch **out, int len, int k, int rows,
                           const unsigned char *gftbls, int nstripes, unsigned char *const *data,
@@ -223,10 +230,37 @@ void isal_hip_multi_partition(long long nstripes, int ndev, int dev, long long *
  * If a HIP call fails during a host-resident call, the call completes on the
  * CPU route and the failure is reported once on stderr; ISAL_HIP_LOG=1 logs
  * every call's route.
+ * Several GPUs: the reference API has no device argument, so a call runs on
+ * the GPU that holds its device-resident (hipMalloc) shards — the thread's
+ * current device is switched to it for the call and restored before the call
+ * returns — else, with no such shard, on the thread's current device. All of
+ * one call's device-resident shards must be on ONE GPU (a call that mixes GPUs
+ * aborts, naming the entry point: no kernel and no CPU route can reach both).
+ * Managed memory runs on either; page-locked host memory is used in place
+ * only on the GPU it was registered with, and staged elsewhere. A thread keeps
+ * one context (stream, buffers, mailbox) per GPU it has called on.
  * Environment knobs are read once; isal_hip_config_reload() re-reads them
  * (call it only while no other thread is inside the library).
  */
 void isal_hip_config_reload(void);
+
+/* The device choice above as a pure function (test hook; the drop-in calls use
+ * it): n shards with kind[i] (ISAL_HIP_MEM_*) and dev[i] (the device their
+ * pointer attributes name; read for DEVICE and PINNED only), the caller's
+ * current device cur. Returns the device the call runs on (-1: none, cur < 0
+ * and no device shard), -2 when device shards are on two GPUs (*bad = the
+ * first shard on a second one; -1 otherwise), -3 for bad arguments.
+ * in_place[i] (optional): 1 where a kernel on that device uses shard i where it
+ * lies, 0 where it must be staged through HBM. */
+#define ISAL_HIP_MEM_PAGEABLE 0
+#define ISAL_HIP_MEM_DEVICE 1
+#define ISAL_HIP_MEM_MANAGED 2
+#define ISAL_HIP_MEM_PINNED 3
+int isal_hip_route_device(int n, const int *kind, const int *dev, int cur, int *bad, int *in_place);
+
+/* Per-thread, per-device contexts the drop-in calls have created since the
+ * process started (a thread's first call on each GPU makes one). */
+unsigned long long isal_hip_contexts_created(void);
 
 /* Drop-in calls served by the CPU route, and of those the HIP-failure
  * fallbacks, since the process started. */
@@ -243,6 +277,13 @@ int isal_hip_max_rows_per_pass(void);
 
 /* Name of the compiled GPU target ("gfx950"). */
 const char *isal_hip_target(void);
+
+/* Ask the HIP runtime for the attributes of every kernel the library's
+ * launchers can launch (each registers itself when the library loads):
+ * returns how many have no usable device code (0: all present; each one is
+ * named on stderr), ISAL_HIP_EHIP without a usable GPU. *nkernels (optional)
+ * receives how many were checked. */
+int isal_hip_selftest_kernels(int *nkernels);
 
 #ifdef __cplusplus
 }

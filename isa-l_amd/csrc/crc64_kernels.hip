@@ -687,7 +687,7 @@ void launch_fused64(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_
   const int ragged = g.tail != 0;
   const size_t lds = static_cast<size_t>(k) * kBlock * 8;
 #define FUSED64_LAUNCH(X0, SL, NV)                                                                 \
-  hipLaunchKernelGGL((ec_encode_crc64_v16<P, U, X0, SL, NV>), dim3((grid + NV - 1) / NV),           \
+  ISAL_LAUNCH((ec_encode_crc64_v16<P, U, X0, SL, NV>), dim3((grid + NV - 1) / NV),           \
                      dim3(kBlock * NV), lds * NV, s, ptrs, ptr_stride, tbl, len, k, nitems,         \
                      static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),                    \
                      static_cast<unsigned>(g.nfull), ragged, xr.src[0], !refl, tabs, part)
@@ -743,11 +743,11 @@ int launch_combine64(const uint64_t* part, const uint64_t* ptrs, int ptr_stride,
   // each combine workgroup copies the 52 KB table set once: cap the grid
   const unsigned grid = nshard < 2048 ? nshard : 2048;
   if (refl)
-    hipLaunchKernelGGL(crc64_combine<true>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
+    ISAL_LAUNCH(crc64_combine<true>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
                        nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
                        tabs, init_term, out, nshard);
   else
-    hipLaunchKernelGGL(crc64_combine<false>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
+    ISAL_LAUNCH(crc64_combine<false>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
                        nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),
                        tabs, init_term, out, nshard);
   isal_hip_count_launch();
@@ -785,11 +785,11 @@ extern "C" int isal_hip_launch_crc64(const uint64_t* d_ptrs, int ptr_stride, int
     if (g.nblk) {
       const unsigned nitems = static_cast<unsigned>(ns * nsh * g.nblk);
       if (vec16)
-        hipLaunchKernelGGL(crc64_shards_pre, dim3((nitems + kPreItems - 1) / kPreItems), dim3(kBlock), 0, s, ptrs,
+        ISAL_LAUNCH(crc64_shards_pre, dim3((nitems + kPreItems - 1) / kPreItems), dim3(kBlock), 0, s, ptrs,
                            ptr_stride, nsh, len, nitems, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
                            static_cast<unsigned>(g.nfull), !refl, d_tabs, part);
       else
-        hipLaunchKernelGGL(crc64_shards_bytes, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, nitems,
+        ISAL_LAUNCH(crc64_shards_bytes, dim3(nitems), dim3(kBlock), 0, s, ptrs, ptr_stride, nsh, len, nitems,
                            static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.tt),
                            static_cast<unsigned>(g.nfull), d_tabs, part);
       isal_hip_count_launch();

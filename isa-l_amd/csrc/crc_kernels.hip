@@ -669,7 +669,7 @@ void launch_fused(unsigned grid, size_t lds, hipStream_t s, const uint64_t* ptrs
                   const isal_hip_crc_geom& g, const isal_hip_xrows& xr, const uint32_t* tabs,
                   uint32_t* part, uint32_t* tail, int nshard_total, int crc_src, int out_shard0) {
 #define FUSED_LAUNCH(REG, SRC, X0, LDS, NB, NV)                                                  \
-  hipLaunchKernelGGL((ec_encode_crc_v16<P, FusedPol<U>, REG, SRC, X0, NB, NV>),                   \
+  ISAL_LAUNCH((ec_encode_crc_v16<P, FusedPol<U>, REG, SRC, X0, NB, NV>),                   \
                      dim3((grid + NV - 1) / NV), dim3(kBlock * NV), (LDS) * NV, s, ptrs, ptr_stride, \
                      src0, dst0, tbl, len, k, nitems, static_cast<unsigned>(g.nblk),               \
                      static_cast<unsigned>(g.tt), static_cast<unsigned>(g.nfull),                  \
@@ -754,12 +754,12 @@ extern "C" int isal_hip_launch_crc(const uint64_t* d_ptrs, int ptr_stride, int i
     uint32_t* part = d_part + static_cast<size_t>(s0) * nshard_total * g.nblk * kBlock;
     uint32_t* tail = d_tail + static_cast<size_t>(s0) * nshard_total * kBlock;
     if (vec16)
-      hipLaunchKernelGGL(crc32c_shards_pre, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
+      ISAL_LAUNCH(crc32c_shards_pre, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
                          ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
                          static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
                          static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
     else
-      hipLaunchKernelGGL(crc32c_shards_bytes, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
+      ISAL_LAUNCH(crc32c_shards_bytes, dim3(crc_grid(nitems)), dim3(kBlock), 0, s, ptrs,
                          ptr_stride, idx0, nsh, len, nitems, static_cast<unsigned>(g.nblk),
                          static_cast<unsigned>(tt), static_cast<unsigned>(g.nfull),
                          static_cast<unsigned>(g.ntiles), d_tabs, part, tail, nshard_total, shard0);
@@ -822,7 +822,7 @@ extern "C" int isal_hip_launch_crc_combine(const uint32_t* d_part, const uint32_
   if (nsh <= 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned grid = nsh < 4096 ? static_cast<unsigned>(nsh) : 4096u;
-  hipLaunchKernelGGL(crc32c_combine, dim3(grid), dim3(kBlock), 0, s, d_part, d_tail, d_plan,
+  ISAL_LAUNCH(crc32c_combine, dim3(grid), dim3(kBlock), 0, s, d_part, d_tail, d_plan,
                      static_cast<unsigned>(nblk), has_tail, init, out, static_cast<unsigned>(nsh));
   isal_hip_count_launch();
   return static_cast<int>(hipGetLastError());

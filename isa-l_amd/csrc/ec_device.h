@@ -10,6 +10,29 @@
 
 namespace {
 
+// Every kernel a host launcher names registers itself when the library loads:
+// ISAL_LAUNCH odr-uses KernelReg<kernel>::id, so each launcher instantiation
+// instantiates the registration with it, and isal_hip_selftest_kernels() asks
+// the runtime for every registered kernel's attributes — a kernel with a host
+// handle but no device code (the r05e abort, DESIGN.md §3 "Kernel registry")
+// is found by a test instead of by a caller's launch.
+template <auto K>
+struct KernelReg {
+  static const int id;
+  static int add() {
+    isal_hip_kreg_add(reinterpret_cast<const void*>(K), __PRETTY_FUNCTION__);
+    return 0;
+  }
+};
+template <auto K>
+const int KernelReg<K>::id = KernelReg<K>::add();
+
+#define ISAL_LAUNCH(kernel, ...)              \
+  do {                                        \
+    (void)KernelReg<kernel>::id;              \
+    hipLaunchKernelGGL(kernel, __VA_ARGS__);  \
+  } while (0)
+
 constexpr int kBlock = 256;           // 4 waves of 64 lanes
 constexpr int kVec = 16;              // bytes per lane per shard
 constexpr int kTile = kBlock * kVec;  // 4 KiB column tile per workgroup step

@@ -113,6 +113,13 @@ __global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encod
 // on the same stream cannot start before this one ends — and writes the
 // result, then the call's sequence number, to the host mailbox. All plain
 // vector memory operations.
+// Memory-model note: the scheme rests on gfx9/CDNA semantics that the HIP
+// memory model does not spell out — vmcnt counts stores and atomics without
+// return, and sc1 stores and agent-scope atomics are performed past the
+// per-XCD L2 — so that a workgroup's relaxed count is ordered after its own
+// results. The last workgroup adds an agent-scope acquire before it reads the
+// verify word the others lowered; on another target this needs a release on
+// every count instead.
 __device__ __forceinline__ void karg_done(const isal_hip_kdone& d, bool tail) {
   if (d.cnt == nullptr) return;  // wave-uniform: the caller synchronises the stream
   if (tail) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -130,6 +137,7 @@ __device__ __forceinline__ void karg_done(const isal_hip_kdone& d, bool tail) {
       __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       unsigned long long r = ~0ull;
       if (d.res != nullptr) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once per call
         r = __hip_atomic_load(d.res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(d.res, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -321,6 +329,11 @@ __global__ __launch_bounds__(kBlock, 4) void ec_encode_glds(const uint64_t* __re
         };
         static_for(step, std::make_integer_sequence<int, R / 2>{});
       }
+      // Every DMA of the item has landed already (the last source's wait is
+      // vmcnt(0)); the explicit drain makes that visible on every path of the
+      // control flow, so the stores and the next item never run inside a
+      // counted window (tests/test_kernel_objects_cpu.py checks the ISA).
+      vm_wait<0>();
 #pragma unroll
       for (int l = 0; l < P; ++l)
         store16<kBufNT>(sp[dst0 + l], off, make_uint4(acc[l][0], acc[l][1], acc[l][2], acc[l][3]), len);
@@ -609,7 +622,7 @@ void launch_glds(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_str
   if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2)
     fprintf(stderr, "isal_hip: kernel ec_encode_glds<%d, %d, %d>\n", P, R, FL);
   const size_t lds = ((static_cast<size_t>(k) * P * 8 + 1023) & ~static_cast<size_t>(1023)) + 4u * R * 1024u;
-  hipLaunchKernelGGL((ec_encode_glds<P, R, FL>), dim3(grid), dim3(kBlock), lds, s, ptrs, ptr_stride, src0, dst0, tbl,
+  ISAL_LAUNCH((ec_encode_glds<P, R, FL>), dim3(grid), dim3(kBlock), lds, s, ptrs, ptr_stride, src0, dst0, tbl,
                      len, k, nitems, tiles, r0m, c0m);
 }
 
@@ -705,7 +718,7 @@ void launch_fl(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_strid
                unsigned c0m) {
   log_launch<P, EncPol<U, kBufNT, kBufNT, 2>, FL>();
   const size_t lds = enc_lds_alloc((FL & kEncLds) ? lds_bytes<P>(k) : 0, P);
-  hipLaunchKernelGGL((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, FL>), dim3(grid), dim3(kBlock), lds, s,
+  ISAL_LAUNCH((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, FL>), dim3(grid), dim3(kBlock), lds, s,
                      ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
 }
 
@@ -744,7 +757,7 @@ hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
       default: launch_v16<P, 4>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, x, r0m, c0m); break;
     }
   } else {
-    hipLaunchKernelGGL(ec_encode_b1<P>, dim3(grid), dim3(kBlock), 0, s, ptrs, ptr_stride, src0,
+    ISAL_LAUNCH(ec_encode_b1<P>, dim3(grid), dim3(kBlock), 0, s, ptrs, ptr_stride, src0,
                        dst0, tbl, len, k, nitems, tiles);
   }
   isal_hip_count_launch();
@@ -760,10 +773,10 @@ hipError_t update_pass(const uint64_t* ptrs, int ptr_stride, int src_idx, int ds
   // (An occupancy cap through dynamic LDS measured flat at 8 workgroups per
   // CU and 2-9 % slower at 4-6, profiles/r04_update_occupancy_ab.jsonl.)
   if (vec16)
-    hipLaunchKernelGGL(ec_update_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
+    ISAL_LAUNCH(ec_update_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
   else
-    hipLaunchKernelGGL(ec_update_b1<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
+    ISAL_LAUNCH(ec_update_b1<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
   isal_hip_count_launch();
   return hipGetLastError();
@@ -858,7 +871,7 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, const isal_hi
     switch (rows) {
 #define EC_KARG4(n)                                                                                           \
   case n:                                                                                                     \
-    hipLaunchKernelGGL((ec_encode_karg4<n>), dim3(blocks), dim3(kBlock), 0, s, *a, *d, len, k);              \
+    ISAL_LAUNCH((ec_encode_karg4<n>), dim3(blocks), dim3(kBlock), 0, s, *a, *d, len, k);              \
     break;
       EC_KARG4(1) EC_KARG4(2) EC_KARG4(3) EC_KARG4(4) EC_KARG4(5) EC_KARG4(6) EC_KARG4(7) EC_KARG4(8)
 #undef EC_KARG4
@@ -876,10 +889,10 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, const isal_hi
 #define EC_KARG(n, u)                                                                                   \
   case n * 16 + u:                                                                                      \
     if (x)                                                                                              \
-      hipLaunchKernelGGL((ec_encode_karg<n, EncPol<u, kBufNT, kBufSC1NT, 2>, kEncXor>), dim3(tiles),      \
+      ISAL_LAUNCH((ec_encode_karg<n, EncPol<u, kBufNT, kBufSC1NT, 2>, kEncXor>), dim3(tiles),      \
                          dim3(kBlock), 0, s, *a, *d, len, k, tiles, r0m, c0m);                          \
     else                                                                                                \
-      hipLaunchKernelGGL((ec_encode_karg<n, EncPol<u, kBufNT, kBufSC1NT, 2>, kEncLUT>), dim3(tiles),      \
+      ISAL_LAUNCH((ec_encode_karg<n, EncPol<u, kBufNT, kBufSC1NT, 2>, kEncLUT>), dim3(tiles),      \
                          dim3(kBlock), 0, s, *a, *d, len, k, tiles, 0ull, 0u);                          \
     break;
 #define EC_KARG_U(n) EC_KARG(n, 12) EC_KARG(n, 10) EC_KARG(n, 8) EC_KARG(n, 6) EC_KARG(n, 5) EC_KARG(n, 4)
@@ -902,7 +915,7 @@ extern "C" int isal_hip_launch_update_karg(const isal_hip_karg* a, const isal_hi
   switch (rows) {
 #define EC_UKARG(n)                                                                                   \
   case n:                                                                                             \
-    hipLaunchKernelGGL(ec_update_karg<n>, dim3(tiles), dim3(kBlock), 0, s, *a, *d, len, tiles);       \
+    ISAL_LAUNCH(ec_update_karg<n>, dim3(tiles), dim3(kBlock), 0, s, *a, *d, len, tiles);       \
     break;
     EC_UKARG(1) EC_UKARG(2) EC_UKARG(3) EC_UKARG(4) EC_UKARG(5) EC_UKARG(6) EC_UKARG(7) EC_UKARG(8)
 #undef EC_UKARG
@@ -925,7 +938,7 @@ template <int P, int U, int FL>
 void launch_verify_v16(unsigned grid, hipStream_t s, const uint64_t* d_ptrs, int ptr_stride, int src_idx0, int dst0,
                        const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long* out,
                        int r0, long long col0, unsigned long long r0m, unsigned c0m, unsigned long long* sbad) {
-  hipLaunchKernelGGL((ec_verify_v16<P, EncPol<U, kBufNT, kBufNT, 0>, FL>), dim3(grid), dim3(kBlock), 0, s, d_ptrs,
+  ISAL_LAUNCH((ec_verify_v16<P, EncPol<U, kBufNT, kBufNT, 0>, FL>), dim3(grid), dim3(kBlock), 0, s, d_ptrs,
                      ptr_stride, src_idx0, dst0, tbl, len, k, nitems, tiles, out, r0, col0, r0m, c0m, sbad);
 }
 
@@ -976,7 +989,7 @@ extern "C" int isal_hip_launch_verify(const uint64_t* d_ptrs, int ptr_stride, in
       switch (P) {
 #define EC_CASE(n)                                                                                      \
   case n:                                                                                               \
-    hipLaunchKernelGGL(ec_verify_b1<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride, src_idx0, dst0, \
+    ISAL_LAUNCH(ec_verify_b1<n>, dim3(grid), dim3(kBlock), 0, s, d_ptrs, ptr_stride, src_idx0, dst0, \
                        tbl, len, k, tiles, tiles, out, r0, col0);                                       \
     break;
         EC_CASE(1) EC_CASE(2) EC_CASE(3) EC_CASE(4) EC_CASE(5) EC_CASE(6) EC_CASE(7) EC_CASE(8)
@@ -1038,11 +1051,11 @@ extern "C" int isal_hip_launch_verify_karg(const isal_hip_karg* a, const isal_hi
   switch (rows * 64 + verify_group(k) * 2 + (x ? 1 : 0)) {
 #define EC_VKARG(n, u)                                                                                             \
   case n * 64 + u * 2:                                                                                             \
-    hipLaunchKernelGGL((ec_verify_karg<n, EncPol<u, kBufNT, kBufNT, 0>, kEncLUT>), dim3(tiles), dim3(kBlock), 0, s, \
+    ISAL_LAUNCH((ec_verify_karg<n, EncPol<u, kBufNT, kBufNT, 0>, kEncLUT>), dim3(tiles), dim3(kBlock), 0, s, \
                        *a, *d, len, k, tiles, 0ull, 0u);                                                           \
     break;                                                                                                         \
   case n * 64 + u * 2 + 1:                                                                                         \
-    hipLaunchKernelGGL((ec_verify_karg<n, EncPol<u, kBufNT, kBufNT, 0>, kEncXor>), dim3(tiles), dim3(kBlock), 0, s, \
+    ISAL_LAUNCH((ec_verify_karg<n, EncPol<u, kBufNT, kBufNT, 0>, kEncXor>), dim3(tiles), dim3(kBlock), 0, s, \
                        *a, *d, len, k, tiles, r0m, c0m);                                                           \
     break;
 #define EC_VKARG_U(n) EC_VKARG(n, 10) EC_VKARG(n, 8) EC_VKARG(n, 6) EC_VKARG(n, 4)

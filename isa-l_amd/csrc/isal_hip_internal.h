@@ -134,15 +134,15 @@ int isal_hip_launch_verify_batch(const uint64_t *d_ptrs, int ptr_stride, int src
                                  const uint32_t *d_tbl, int len, int k, int rows, long long nstripes,
                                  const isal_hip_encmask *em, unsigned long long *bad, void *stream);
 
-/* The shim's generic synchronous call (host or device shard pointers).
- * op: ISAL_HIP_OP_ENCODE (dst = coded sources, nsrc = k), ISAL_HIP_OP_UPDATE
+/* The shim's generic synchronous call (host or device shard pointers); fn
+ * names the entry point in abort messages. op: ISAL_HIP_OP_ENCODE (dst = coded sources, nsrc = k), ISAL_HIP_OP_UPDATE
  * (dst ^= c[.][vec_i] * src[0], nsrc = 1), ISAL_HIP_OP_VERIFY (compare dst
  * with the coded sources). Returns ~0, or for VERIFY the first mismatch as
  * column << 8 | row. */
 #define ISAL_HIP_OP_ENCODE 0
 #define ISAL_HIP_OP_UPDATE 1
 #define ISAL_HIP_OP_VERIFY 2
-unsigned long long isal_hip_run(int op, int len, int k, int rows, int vec_i,
+unsigned long long isal_hip_run(const char *fn, int op, int len, int k, int rows, int vec_i,
                                 const unsigned char *gftbls, unsigned char *const *src, int nsrc,
                                 unsigned char *const *dst);
 
@@ -158,6 +158,17 @@ typedef struct {
         unsigned long long src[EC_MAX_ROWS_PER_PASS];
 } isal_hip_xrows;
 void isal_hip_xor_rows(int k, int rows, const unsigned char *gftbls, isal_hip_xrows *x);
+
+/* Make dev the calling thread's current device for a call on an object that
+ * belongs to it; returns what isal_hip_dev_leave restores (-1: nothing, -2:
+ * the switch failed). */
+int isal_hip_dev_enter(int dev);
+void isal_hip_dev_leave(int prev);
+
+/* Kernel registry (isal_hip_selftest_kernels): every kernel a launcher can
+ * launch registers its host handle and a name when the library loads
+ * (ec_device.h ISAL_LAUNCH). */
+void isal_hip_kreg_add(const void *fn, const char *name);
 
 /* Launch counter shared by the shim and the launchers. */
 void isal_hip_count_launch(void);

@@ -11,6 +11,7 @@
  * mechanism off for an A/B or a fallback, or exists for a test.
  */
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -69,12 +70,46 @@ parse(const knob_def *d)
         return -2; /* set, but not a known word */
 }
 
+/* ISAL_HIP_* names the library reads that are not knobs of the table */
+static const char *const other_names[] = {"ISAL_HIP_SYSFS_ROOT", "ISAL_HIP_LIB", NULL};
+
+extern char **environ;
+
+/* An ISAL_HIP_* variable the library does not read — a knob removed in an
+ * earlier round, or a typo — would silently leave an A/B arm on the default:
+ * say so once per process, naming each such variable. */
+static void
+warn_unknown(void)
+{
+        static int warned;
+        char **e;
+        if (__atomic_exchange_n(&warned, 1, __ATOMIC_RELAXED) || !environ)
+                return;
+        for (e = environ; *e; e++) {
+                const char *v = *e, *eq = strchr(v, '=');
+                size_t n;
+                int i, known = 0;
+                if (strncmp(v, "ISAL_HIP_", 9) != 0 || !eq)
+                        continue;
+                n = (size_t) (eq - v);
+                for (i = 0; i < ISAL_HIP_KNOB_COUNT && !known; i++)
+                        known = strlen(defs[i].name) == n && strncmp(defs[i].name, v, n) == 0;
+                for (i = 0; other_names[i] && !known; i++)
+                        known = strlen(other_names[i]) == n && strncmp(other_names[i], v, n) == 0;
+                if (!known)
+                        fprintf(stderr, "isal_hip: ignoring unknown environment variable %.*s (not a knob of this "
+                                        "library; see isal_hip_knobs.c)\n",
+                                (int) n, v);
+        }
+}
+
 static void
 load(void)
 {
         int i;
         for (i = 0; i < ISAL_HIP_KNOB_COUNT; i++)
                 values[i] = parse(&defs[i]);
+        warn_unknown();
 }
 
 long long

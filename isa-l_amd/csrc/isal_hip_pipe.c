@@ -123,8 +123,8 @@ isal_hip_pipe_create(isal_hip_pipe **out, int len, int k, int rows, const unsign
         return ISAL_HIP_OK;
 }
 
-int
-isal_hip_pipe_submit(isal_hip_pipe *p, unsigned char *const *data, unsigned char *const *coding)
+static int
+pipe_submit_impl(isal_hip_pipe *p, unsigned char *const *data, unsigned char *const *coding)
 {
         int slot, j, l, stride, vec16;
         unsigned char *base;
@@ -186,8 +186,8 @@ isal_hip_pipe_submit(isal_hip_pipe *p, unsigned char *const *data, unsigned char
         return ISAL_HIP_OK;
 }
 
-int
-isal_hip_pipe_flush(isal_hip_pipe *p)
+static int
+pipe_flush_impl(isal_hip_pipe *p)
 {
         if (!p)
                 return ISAL_HIP_EINVAL;
@@ -233,4 +233,32 @@ isal_hip_pipe_destroy(isal_hip_pipe *p)
         free(p->slot_used);
         free(p);
         return ISAL_HIP_OK;
+}
+
+/* the pipeline's calls run on its device (its streams and buffers are there) */
+int
+isal_hip_pipe_submit(isal_hip_pipe *p, unsigned char *const *data, unsigned char *const *coding)
+{
+        int prev, r;
+        if (!p)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(p->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = pipe_submit_impl(p, data, coding);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+/* the pipeline's calls run on its device (its streams and buffers are there) */
+int
+isal_hip_pipe_flush(isal_hip_pipe *p)
+{
+        int prev, r;
+        if (!p)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(p->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = pipe_flush_impl(p);
+        isal_hip_dev_leave(prev);
+        return r;
 }

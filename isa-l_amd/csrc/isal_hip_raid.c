@@ -69,14 +69,14 @@ raid_tables(int n, int rows, int *owned)
 }
 
 static int
-raid_run(int op, int len, int nsrc, int rows, void **array)
+raid_run(const char *fn, int op, int len, int nsrc, int rows, void **array)
 {
         int owned;
         const unsigned char *t = raid_tables(nsrc, rows, &owned);
         unsigned long long bad;
         if (!t)
                 return 1;
-        bad = isal_hip_run(op, len, nsrc, rows, 0, t, (unsigned char *const *) array, nsrc,
+        bad = isal_hip_run(fn, op, len, nsrc, rows, 0, t, (unsigned char *const *) array, nsrc,
                            (unsigned char *const *) array + nsrc);
         if (owned)
                 free((void *) t);
@@ -91,7 +91,7 @@ xor_gen(int vects, int len, void **array)
 {
         if (vects < 3)
                 return 1;
-        return raid_run(ISAL_HIP_OP_ENCODE, len, vects - 1, 1, array);
+        return raid_run("xor_gen", ISAL_HIP_OP_ENCODE, len, vects - 1, 1, array);
 }
 
 int
@@ -106,7 +106,7 @@ xor_check(int vects, int len, void **array)
         if (vects < 2)
                 return 1;
         /* XOR of all == 0  <=>  XOR of the first vects-1 equals the last */
-        return raid_run(ISAL_HIP_OP_VERIFY, len, vects - 1, 1, array) ? 1 : 0;
+        return raid_run("xor_check", ISAL_HIP_OP_VERIFY, len, vects - 1, 1, array) ? 1 : 0;
 }
 
 int
@@ -124,7 +124,7 @@ pq_gen(int vects, int len, void **array)
                 return 0;
         if (len % 32)
                 return 1;
-        return raid_run(ISAL_HIP_OP_ENCODE, len, vects - 2, 2, array);
+        return raid_run("pq_gen", ISAL_HIP_OP_ENCODE, len, vects - 2, 2, array);
 }
 
 int
@@ -132,7 +132,7 @@ pq_gen_base(int vects, int len, void **array)
 {
         if (vects < 4)
                 return 1;
-        return raid_run(ISAL_HIP_OP_ENCODE, len & ~7, vects - 2, 2, array);
+        return raid_run("pq_gen_base", ISAL_HIP_OP_ENCODE, len & ~7, vects - 2, 2, array);
 }
 
 int
@@ -140,7 +140,7 @@ pq_check(int vects, int len, void **array)
 {
         if (vects < 4)
                 return 1;
-        return raid_run(ISAL_HIP_OP_VERIFY, len, vects - 2, 2, array);
+        return raid_run("pq_check", ISAL_HIP_OP_VERIFY, len, vects - 2, 2, array);
 }
 
 int

@@ -29,6 +29,8 @@
  * Thread safety: all mutable state is per thread (pthread key) except the
  * atomic counters and the read-once knobs.
  */
+#define _GNU_SOURCE /* dladdr */
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 #include <sched.h>
@@ -78,6 +80,59 @@ unsigned long long
 isal_hip_fallbacks(void)
 {
         return __atomic_load_n(&g_fallbacks, __ATOMIC_RELAXED);
+}
+
+/* ---- kernel registry --------------------------------------------------------
+ * Filled while the library loads (static initialisers of the kernel objects,
+ * ec_device.h KernelReg), read by isal_hip_selftest_kernels. */
+#define KREG_MAX 4096
+static int gpu_present(void);
+static const void *kreg_fn[KREG_MAX];
+static const char *kreg_name[KREG_MAX];
+static int kreg_n, kreg_lost;
+
+void
+isal_hip_kreg_add(const void *fn, const char *name)
+{
+        const int i = __atomic_fetch_add(&kreg_n, 1, __ATOMIC_RELAXED);
+        if (i >= KREG_MAX) {
+                __atomic_add_fetch(&kreg_lost, 1, __ATOMIC_RELAXED);
+                return;
+        }
+        kreg_fn[i] = fn;
+        kreg_name[i] = name;
+}
+
+int
+isal_hip_selftest_kernels(int *nkernels)
+{
+        int i, n = __atomic_load_n(&kreg_n, __ATOMIC_ACQUIRE), bad = 0;
+        if (n > KREG_MAX)
+                n = KREG_MAX;
+        if (nkernels)
+                *nkernels = n;
+        if (__atomic_load_n(&kreg_lost, __ATOMIC_RELAXED))
+                return ISAL_HIP_ENOMEM; /* the registry is too small to vouch for every kernel */
+        if (!gpu_present())
+                return ISAL_HIP_EHIP;
+        for (i = 0; i < n; i++) {
+                hipFuncAttributes a;
+                const hipError_t e = hipFuncGetAttributes(&a, kreg_fn[i]);
+                if (e != hipSuccess) {
+                        Dl_info info;
+                        const int found = dladdr(kreg_fn[i], &info) != 0;
+                        (void) hipGetLastError();
+                        fprintf(stderr,
+                                "isal_hip: selftest: kernel with no usable device code: %s (handle %s+0x%lx): "
+                                "%s\n",
+                                kreg_name[i], found ? info.dli_fname : "?",
+                                found ? (unsigned long) ((const char *) kreg_fn[i] - (const char *) info.dli_fbase)
+                                      : 0ul,
+                                hipGetErrorString(e));
+                        bad++;
+                }
+        }
+        return bad;
 }
 
 int
@@ -279,10 +334,25 @@ static void outq_stop(ctx_t *c);
 static pthread_key_t ctx_key;
 static pthread_once_t ctx_once = PTHREAD_ONCE_INIT;
 
-static void
-ctx_release(void *p)
+/* A calling thread's contexts, one per device it has made calls on: a thread
+ * that serves shards on several GPUs keeps each GPU's stream, buffers and
+ * mailbox instead of rebuilding them on every device switch. */
+#define CTX_MAX_DEV 64
+typedef struct {
+        ctx_t *dev[CTX_MAX_DEV];
+} tctx_t;
+
+static unsigned long long g_ctx_created;
+
+unsigned long long
+isal_hip_contexts_created(void)
 {
-        ctx_t *c = (ctx_t *) p;
+        return __atomic_load_n(&g_ctx_created, __ATOMIC_RELAXED);
+}
+
+static void
+ctx_free(ctx_t *c)
+{
         if (!c)
                 return;
         /* Best effort at thread exit: the runtime may already be shutting down. */
@@ -317,48 +387,66 @@ ctx_release(void *p)
 }
 
 static void
+tctx_release(void *p)
+{
+        tctx_t *t = (tctx_t *) p;
+        int d;
+        if (!t)
+                return;
+        for (d = 0; d < CTX_MAX_DEV; d++)
+                ctx_free(t->dev[d]);
+        free(t);
+}
+
+static void
 ctx_key_init(void)
 {
-        if (pthread_key_create(&ctx_key, ctx_release) != 0) {
+        if (pthread_key_create(&ctx_key, tctx_release) != 0) {
                 fprintf(stderr, "isal_hip: pthread_key_create failed\n");
                 abort();
         }
 }
 
-/* The calling thread's context on the current device, or NULL with *err set. */
+/* The calling thread's context on device dev — which must be the thread's
+ * current device when the context is first made (its stream belongs to the
+ * current device) — or NULL with *err set. */
 static ctx_t *
-ctx_get(hipError_t *err, const char **what)
+ctx_get(int dev, hipError_t *err, const char **what)
 {
+        tctx_t *t;
         ctx_t *c;
-        int dev;
         pthread_once(&ctx_once, ctx_key_init);
-        if ((*err = hipGetDevice(&dev)) != hipSuccess) {
-                *what = "hipGetDevice";
+        if (dev < 0 || dev >= CTX_MAX_DEV) {
+                *err = hipErrorInvalidDevice;
+                *what = "device ordinal (at most 64 GPUs per process)";
                 return NULL;
         }
-        c = (ctx_t *) pthread_getspecific(ctx_key);
-        if (c && c->device != dev) {
-                ctx_release(c);
-                pthread_setspecific(ctx_key, NULL);
-                c = NULL;
-        }
-        if (!c) {
-                c = (ctx_t *) calloc(1, sizeof(*c));
-                if (!c) {
+        t = (tctx_t *) pthread_getspecific(ctx_key);
+        if (!t) {
+                t = (tctx_t *) calloc(1, sizeof(*t));
+                if (!t || pthread_setspecific(ctx_key, t) != 0) {
                         fprintf(stderr, "isal_hip: out of host memory\n");
                         abort();
                 }
-                c->device = dev;
-                /* A BLOCKING stream: it is ordered after work already queued on the
-                 * legacy default stream (e.g. torch kernels that just wrote the
-                 * shards), as the synchronous reference API implies. */
-                if ((*err = hipStreamCreate(&c->stream)) != hipSuccess) {
-                        *what = "hipStreamCreate";
-                        free(c);
-                        return NULL;
-                }
-                pthread_setspecific(ctx_key, c);
         }
+        if ((c = t->dev[dev]) != NULL)
+                return c;
+        c = (ctx_t *) calloc(1, sizeof(*c));
+        if (!c) {
+                fprintf(stderr, "isal_hip: out of host memory\n");
+                abort();
+        }
+        c->device = dev;
+        /* A BLOCKING stream: it is ordered after work already queued on the
+         * legacy default stream (e.g. torch kernels that just wrote the
+         * shards), as the synchronous reference API implies. */
+        if ((*err = hipStreamCreate(&c->stream)) != hipSuccess) {
+                *what = "hipStreamCreate";
+                free(c);
+                return NULL;
+        }
+        t->dev[dev] = c;
+        __atomic_add_fetch(&g_ctx_created, 1ull, __ATOMIC_RELAXED);
         return c;
 }
 
@@ -492,26 +580,32 @@ stage_limit(void)
 
 /* ---- pointer classification ------------------------------------------- */
 
-/* Where a shard lives, as the kernels see it. Device (hipMalloc) and managed
- * memory: the pointer itself. Page-locked host memory (hipHostMalloc,
- * hipHostRegister — NIC / disk DMA buffers usually are): the device's mapping
- * of it, so kernels read and write it in place over PCIe with no staging copy
+/* Where a shard lives (kind; ISAL_HIP_MEM_*) and, for device and page-locked
+ * memory, the device its attributes name (*dev; -1 otherwise). Returns what a
+ * kernel would use for it: device (hipMalloc) and managed memory, the pointer
+ * itself; page-locked host memory (hipHostMalloc, hipHostRegister — NIC / disk
+ * DMA buffers usually are), the device's mapping of it, which kernels of THAT
+ * device read and write in place over PCIe with no staging copy
  * (ISAL_HIP_PINNED_DIRECT=0 stages it like pageable memory) — but only when
  * the shard's LAST byte maps through the same registration too: a shard that
- * runs past the end of a partly registered buffer would make the kernel
- * touch unmapped memory (a GPU fault the CPU route could not recover from),
- * so it is staged. Pageable memory: 0 — it must be copied through a staging
- * buffer. *kind: CL_HOST (pageable or page-locked host memory), CL_DEVICE
- * (hipMalloc memory: *rbase / *rsize receive its allocation's range) or
- * CL_MANAGED — device-visible memory that no CPU route can read. */
-enum { CL_HOST = 0, CL_DEVICE = 1, CL_MANAGED = 2 };
+ * runs past the end of a partly registered buffer would make the kernel touch
+ * unmapped memory (a GPU fault the CPU route could not recover from), so it is
+ * staged (kind pageable). Pageable memory: 0 — it is copied through a staging
+ * buffer. For device memory *rbase / *rsize receive its allocation's range. */
+enum {
+        CL_HOST = ISAL_HIP_MEM_PAGEABLE,
+        CL_DEVICE = ISAL_HIP_MEM_DEVICE,
+        CL_MANAGED = ISAL_HIP_MEM_MANAGED,
+        CL_PINNED = ISAL_HIP_MEM_PINNED,
+};
 
 static uint64_t
-classify(const void *p, size_t len, int dev, int *kind, uintptr_t *rbase, size_t *rsize)
+classify(const void *p, size_t len, int *kind, int *dev, uintptr_t *rbase, size_t *rsize)
 {
         hipPointerAttribute_t a, z;
         hipError_t e;
         *kind = CL_HOST;
+        *dev = -1;
         *rsize = 0;
         if (!p)
                 return 0;
@@ -524,6 +618,7 @@ classify(const void *p, size_t len, int dev, int *kind, uintptr_t *rbase, size_t
                 hipDeviceptr_t base;
                 size_t size;
                 *kind = CL_DEVICE;
+                *dev = a.device;
                 if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t) p) == hipSuccess) {
                         *rbase = (uintptr_t) base;
                         *rsize = size;
@@ -536,25 +631,59 @@ classify(const void *p, size_t len, int dev, int *kind, uintptr_t *rbase, size_t
                 *kind = CL_MANAGED;
                 return (uint64_t) (uintptr_t) p;
         }
-        if (a.type == hipMemoryTypeHost && a.devicePointer && a.device == dev &&
+        if (a.type == hipMemoryTypeHost && a.devicePointer &&
             isal_hip_knob(ISAL_HIP_KNOB_PINNED_DIRECT) != 0) {
                 /* attributes describe p itself (the mapping of the allocation
-                 * base plus p's offset into it). Only the mapping made for the
-                 * calling thread's device is used; page-locked memory of
-                 * another device is staged. */
+                 * base plus p's offset into it) */
                 const char *last = (const char *) p + (len ? len - 1 : 0);
                 if (len > 1) {
                         if (hipPointerGetAttributes(&z, last) != hipSuccess) {
                                 (void) hipGetLastError();
                                 return 0;
                         }
-                        if (z.type != hipMemoryTypeHost || z.device != dev ||
+                        if (z.type != hipMemoryTypeHost || z.device != a.device ||
                             (const char *) z.devicePointer != (const char *) a.devicePointer + (len - 1))
                                 return 0;
                 }
+                *kind = CL_PINNED;
+                *dev = a.device;
                 return (uint64_t) (uintptr_t) a.devicePointer;
         }
         return 0;
+}
+
+/* The device a drop-in call runs on (isal_hip.h). The reference API has no
+ * device argument (erasure_code.h:108-110), so it comes from the shards: the
+ * device that holds the call's device-resident (hipMalloc) shards — they must
+ * all be on one; managed memory does not bind a device — else the caller's
+ * current device. A page-locked host shard is used in place only through the
+ * mapping made for the chosen device (its own); otherwise it is staged. */
+int
+isal_hip_route_device(int n, const int *kind, const int *dev, int cur, int *bad, int *in_place)
+{
+        int i, owner = -1;
+        if (bad)
+                *bad = -1;
+        if (n < 0 || (n > 0 && (!kind || !dev)))
+                return -3;
+        for (i = 0; i < n; i++) {
+                if (kind[i] != CL_DEVICE)
+                        continue;
+                if (owner < 0) {
+                        owner = dev[i];
+                } else if (dev[i] != owner) {
+                        if (bad)
+                                *bad = i;
+                        return -2;
+                }
+        }
+        if (owner < 0)
+                owner = cur;
+        if (in_place)
+                for (i = 0; i < n; i++)
+                        in_place[i] = kind[i] == CL_DEVICE || kind[i] == CL_MANAGED ||
+                                      (kind[i] == CL_PINNED && owner >= 0 && dev[i] == owner);
+        return owner;
 }
 
 /* Device allocations already seen by one call: a shard inside one of them is
@@ -565,25 +694,28 @@ classify(const void *p, size_t len, int dev, int *kind, uintptr_t *rbase, size_t
 typedef struct {
         int n;
         uintptr_t lo[SEEN_MAX], hi[SEEN_MAX];
+        int dev[SEEN_MAX];
 } seen_t;
 
+/* the device of the seen allocation holding [p, p + len), or -1 */
 static int
-seen_has(const seen_t *sn, const void *p, size_t len)
+seen_dev(const seen_t *sn, const void *p, size_t len)
 {
         const uintptr_t a = (uintptr_t) p;
         int i;
         for (i = 0; i < sn->n; i++)
                 if (a >= sn->lo[i] && a < sn->hi[i] && len <= sn->hi[i] - a)
-                        return 1;
-        return 0;
+                        return sn->dev[i];
+        return -1;
 }
 
 static void
-seen_add(seen_t *sn, uintptr_t base, size_t size)
+seen_add(seen_t *sn, uintptr_t base, size_t size, int dev)
 {
-        if (size && sn->n < SEEN_MAX) {
+        if (size && dev >= 0 && sn->n < SEEN_MAX) {
                 sn->lo[sn->n] = base;
                 sn->hi[sn->n] = base + size;
+                sn->dev[sn->n] = dev;
                 sn->n++;
         }
 }
@@ -1503,11 +1635,17 @@ gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *
          const isal_hip_encmask *em, int mail)
 {
         static int inflight; /* kernel-argument calls of the process in flight (lane width) */
+        static const char *const launch_what[] = {"encode launch (kernel arguments)",
+                                                  "update launch (kernel arguments)",
+                                                  "verify launch (kernel arguments)"};
+        static const char *const wait_what[] = {"encode completion (kernel arguments)",
+                                                "update completion (kernel arguments)",
+                                                "verify completion (kernel arguments)"};
         gpu_res r = {hipSuccess, NULL, 0, 0, 0, ~0ull};
         const int nsrc = op == OP_UPDATE ? 1 : k;
         isal_hip_kdone d = {NULL, NULL, NULL, 0ull};
         isal_hip_karg a;
-        hipError_t karg_launch, karg_wait;
+        hipError_t e;
         int busy;
         memset(&a, 0, sizeof(a));
         memcpy(a.ptrs, view, sizeof(uint64_t) * (size_t) (nsrc + rows));
@@ -1516,29 +1654,39 @@ gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *
                 d.cnt = (unsigned *) c->d_done;
                 d.res = op == OP_VERIFY ? (unsigned long long *) ((char *) c->d_done + KDONE_CNT_BYTES) : NULL;
                 d.mail = (unsigned long long *) c->h_mail_dev;
-                d.seq = ++c->seq;
         }
+        /* an injected launch failure (tests) launches nothing, as a failed launch */
+        if (fault_at(FAULT_LAUNCH, 0)) {
+                r.err = hipErrorOutOfMemory;
+                r.what = launch_what[op];
+                return r;
+        }
+        if (mail)
+                d.seq = ++c->seq;
         if (op == OP_UPDATE) {
                 /* one pass: source vec_i's tables for every row are contiguous */
                 memcpy(a.tbl, tbl + isal_hip_tables_dwords(vec_i, rows), isal_hip_tables_dwords(1, rows) * 4);
-                karg_launch = (hipError_t) isal_hip_launch_update_karg(&a, &d, len, rows, c->stream);
+                e = (hipError_t) isal_hip_launch_update_karg(&a, &d, len, rows, c->stream);
         } else {
                 memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
                 busy = __atomic_add_fetch(&inflight, 1, __ATOMIC_RELAXED);
-                karg_launch = (hipError_t) (op == OP_VERIFY
-                                          ? isal_hip_launch_verify_karg(&a, &d, len, k, rows, em, c->stream)
-                                          : isal_hip_launch_encode_karg(&a, &d, len, k, rows, em, busy, c->stream));
+                e = (hipError_t) (op == OP_VERIFY ? isal_hip_launch_verify_karg(&a, &d, len, k, rows, em, c->stream)
+                                                  : isal_hip_launch_encode_karg(&a, &d, len, k, rows, em, busy,
+                                                                                c->stream));
         }
-        if (karg_launch == hipSuccess && fault_at(FAULT_LAUNCH, 0))
-                karg_launch = hipErrorOutOfMemory; /* injected (tests) */
-        karg_wait = karg_launch != hipSuccess ? karg_launch
-                    : fault_at(FAULT_SYNC, 0) ? hipErrorOutOfMemory
-                    : mail                    ? wait_done(c, d.seq)
-                                              : hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) {
+                r.what = wait_what[op];
+                e = fault_at(FAULT_SYNC, 0) ? hipErrorOutOfMemory
+                    : mail                  ? wait_done(c, d.seq)
+                                            : hipStreamSynchronize(c->stream);
+        } else {
+                r.what = launch_what[op];
+        }
         if (op != OP_UPDATE) /* this call is no longer in flight, whatever failed */
                 __atomic_sub_fetch(&inflight, 1, __ATOMIC_RELAXED);
-        GPU_TRY(r, karg_launch);
-        GPU_TRY(r, karg_wait);
+        if ((r.err = e) != hipSuccess)
+                return r;
+        r.what = NULL;
         if (op == OP_VERIFY)
                 r.first_bad = c->h_mail[1];
         r.done = len;
@@ -1553,25 +1701,41 @@ cpu_route(int op, long long c0, int len, int k, int rows, int vec_i, const unsig
         return isal_cpu_run(op, c0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
 }
 
+/* A call whose device-resident shards sit on two GPUs: no one kernel can
+ * reach both (and no CPU route can read either). */
+static void
+die_mixed(const char *fn, int i0, int d0, int i1, int d1)
+{
+        fprintf(stderr,
+                "isal_hip: %s: device-resident shards on two GPUs (shard %d on device %d, shard %d "
+                "on device %d); one call runs on one GPU, aborting\n",
+                fn, i0, d0, i1, d1);
+        abort();
+}
+
 /*
  * OP_ENCODE: dst[l] = XOR_j c[l][j] * src[j], nsrc = k.
  * OP_UPDATE: dst[l] ^= c[l][vec_i] * src[0], nsrc = 1.
  * OP_VERIFY: compare dst[l] with XOR_j c[l][j] * src[j]; nothing is written.
  * Returns ~0 (no mismatch / not a verify) or the first mismatch as
- * column << 8 | row.
+ * column << 8 | row. fn names the entry point in abort messages.
+ * The call runs on the device holding its device-resident shards
+ * (isal_hip_route_device): the thread's current device is switched to it for
+ * the call and restored before returning.
  */
 static unsigned long long
-run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+run_ec(const char *fn, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
        unsigned char *const *src, int nsrc, unsigned char *const *dst)
 {
         const int be = backend();
         const int nptr = nsrc + rows;
         uint64_t view_buf[512], *view;
+        int kind_buf[512], dev_buf[512], *kind, *devs;
         static const isal_hip_encmask no_masks;
         const isal_hip_encmask *em = &no_masks;
         const uint32_t *tbl = NULL;
         seen_t sn;
-        int i, nstage = 0, ndev = 0, nplain = 0, all_host, cur_dev, mail;
+        int i, nstage = 0, ndev = 0, nplain = 0, all_host, cur_dev, run_dev, bad, mail;
         size_t bytes;
         gpu_res r;
         ctx_t *c;
@@ -1596,10 +1760,18 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 return cpu_route(op, 0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
         }
 
-        view = nptr <= 512 ? view_buf : (uint64_t *) malloc(sizeof(uint64_t) * (size_t) nptr);
-        if (!view) {
-                fprintf(stderr, "isal_hip: out of host memory\n");
-                abort();
+        if (nptr <= 512) {
+                view = view_buf;
+                kind = kind_buf;
+                devs = dev_buf;
+        } else {
+                view = (uint64_t *) malloc((sizeof(uint64_t) + 2 * sizeof(int)) * (size_t) nptr);
+                if (!view) {
+                        fprintf(stderr, "isal_hip: out of host memory\n");
+                        abort();
+                }
+                kind = (int *) (view + nptr);
+                devs = kind + nptr;
         }
         if (hipGetDevice(&cur_dev) != hipSuccess) {
                 (void) hipGetLastError();
@@ -1608,18 +1780,35 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         sn.n = 0;
         for (i = 0; i < nptr; i++) {
                 const void *p = i < nsrc ? src[i] : dst[i - nsrc];
-                int is_dev, kind = CL_DEVICE;
                 uintptr_t rb = 0;
                 size_t rs = 0;
-                if (seen_has(&sn, p, (size_t) len)) {
+                const int sd = seen_dev(&sn, p, (size_t) len);
+                if (sd >= 0) {
                         view[i] = (uint64_t) (uintptr_t) p;
+                        kind[i] = CL_DEVICE;
+                        devs[i] = sd;
                 } else {
-                        view[i] = classify(p, (size_t) len, cur_dev, &kind, &rb, &rs);
-                        if (kind == CL_DEVICE)
-                                seen_add(&sn, rb, rs);
+                        view[i] = classify(p, (size_t) len, &kind[i], &devs[i], &rb, &rs);
+                        if (kind[i] == CL_DEVICE)
+                                seen_add(&sn, rb, rs, devs[i]);
                 }
-                is_dev = kind != CL_HOST;
-                nplain += kind == CL_DEVICE;
+        }
+        /* the device the call runs on (-1: none known, the caller's current
+         * device could not be read) */
+        run_dev = isal_hip_route_device(nptr, kind, devs, cur_dev, &bad, NULL);
+        if (run_dev == -2) {
+                int i0 = 0;
+                while (kind[i0] != CL_DEVICE)
+                        i0++;
+                die_mixed(fn, i0, devs[i0], bad, devs[bad]);
+        }
+        for (i = 0; i < nptr; i++) {
+                const int is_dev = kind[i] == CL_DEVICE || kind[i] == CL_MANAGED;
+                /* page-locked memory is used in place only through the run
+                 * device's own mapping */
+                if (kind[i] == CL_PINNED && devs[i] != run_dev)
+                        view[i] = 0;
+                nplain += kind[i] == CL_DEVICE;
                 /* An update's parity in page-locked host memory is staged, not
                  * written in place: a kernel that failed after it started could
                  * have folded some of it already, and the CPU fallback could not
@@ -1640,7 +1829,10 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
                 return cpu_route(op, 0, len, k, rows, vec_i, gftbls, src, nsrc, dst);
         }
 
-        c = ctx_get(&r.err, &r.what);
+        /* the shards' device, when the caller's current device is another one */
+        if (run_dev != cur_dev && (r.err = hipSetDevice(run_dev)) != hipSuccess)
+                die("hipSetDevice (to the device holding the shards)", r.err);
+        c = ctx_get(run_dev, &r.err, &r.what);
         if (c && !(tbl = ctx_tables(c, k, rows, gftbls, &em))) {
                 r.err = hipErrorOutOfMemory;
                 r.what = "ctx_tables (host memory)";
@@ -1671,10 +1863,14 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
         }
         if (view != view_buf)
                 free(view);
-        if (r.err == hipSuccess)
+        if (r.err == hipSuccess) {
+                if (run_dev != cur_dev)
+                        (void) hipSetDevice(cur_dev);
                 return r.first_bad;
+        }
         if (!all_host || be == BACKEND_GPU)
                 die(r.what, r.err);
+        /* all shards host-resident: the call ran on the caller's own device */
         (void) hipGetLastError();
         report_fallback(r.what, r.err);
         /* Nothing queued may still write our outputs: drain every stream of the
@@ -1701,10 +1897,10 @@ run_ec(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
 }
 
 unsigned long long
-isal_hip_run(int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
+isal_hip_run(const char *fn, int op, int len, int k, int rows, int vec_i, const unsigned char *gftbls,
              unsigned char *const *src, int nsrc, unsigned char *const *dst)
 {
-        return run_ec(op, len, k, rows, vec_i, gftbls, src, nsrc, dst);
+        return run_ec(fn, op, len, k, rows, vec_i, gftbls, src, nsrc, dst);
 }
 
 /* ---- reference data-path ABI ------------------------------------------- */
@@ -1713,56 +1909,56 @@ void
 ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
                unsigned char **coding)
 {
-        run_ec(OP_ENCODE, len, k, rows, 0, gftbls, data, k, coding);
+        run_ec("ec_encode_data", OP_ENCODE, len, k, rows, 0, gftbls, data, k, coding);
 }
 
 void
 ec_encode_data_base(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
                     unsigned char **coding)
 {
-        run_ec(OP_ENCODE, len, k, rows, 0, gftbls, data, k, coding);
+        run_ec("ec_encode_data_base", OP_ENCODE, len, k, rows, 0, gftbls, data, k, coding);
 }
 
 void
 ec_encode_data_update(int len, int k, int rows, int vec_i, unsigned char *gftbls,
                       unsigned char *data, unsigned char **coding)
 {
-        run_ec(OP_UPDATE, len, k, rows, vec_i, gftbls, &data, 1, coding);
+        run_ec("ec_encode_data_update", OP_UPDATE, len, k, rows, vec_i, gftbls, &data, 1, coding);
 }
 
 void
 ec_encode_data_update_base(int len, int k, int rows, int vec_i, unsigned char *gftbls,
                            unsigned char *data, unsigned char **coding)
 {
-        run_ec(OP_UPDATE, len, k, rows, vec_i, gftbls, &data, 1, coding);
+        run_ec("ec_encode_data_update_base", OP_UPDATE, len, k, rows, vec_i, gftbls, &data, 1, coding);
 }
 
 void
 gf_vect_dot_prod(int len, int vlen, unsigned char *gftbls, unsigned char **src,
                  unsigned char *dest)
 {
-        run_ec(OP_ENCODE, len, vlen, 1, 0, gftbls, src, vlen, &dest);
+        run_ec("gf_vect_dot_prod", OP_ENCODE, len, vlen, 1, 0, gftbls, src, vlen, &dest);
 }
 
 void
 gf_vect_dot_prod_base(int len, int vlen, unsigned char *gftbls, unsigned char **src,
                       unsigned char *dest)
 {
-        run_ec(OP_ENCODE, len, vlen, 1, 0, gftbls, src, vlen, &dest);
+        run_ec("gf_vect_dot_prod_base", OP_ENCODE, len, vlen, 1, 0, gftbls, src, vlen, &dest);
 }
 
 void
 gf_vect_mad(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src,
             unsigned char *dest)
 {
-        run_ec(OP_UPDATE, len, vec, 1, vec_i, gftbls, &src, 1, &dest);
+        run_ec("gf_vect_mad", OP_UPDATE, len, vec, 1, vec_i, gftbls, &src, 1, &dest);
 }
 
 void
 gf_vect_mad_base(int len, int vec, int vec_i, unsigned char *gftbls, unsigned char *src,
                  unsigned char *dest)
 {
-        run_ec(OP_UPDATE, len, vec, 1, vec_i, gftbls, &src, 1, &dest);
+        run_ec("gf_vect_mad_base", OP_UPDATE, len, vec, 1, vec_i, gftbls, &src, 1, &dest);
 }
 
 /* dest = c * src with c = gftbl[1]; -1 (nothing touched) when len % 32 != 0,
@@ -1773,7 +1969,7 @@ gf_vect_mul(int len, unsigned char *gftbl, void *src, void *dest)
         unsigned char *s = (unsigned char *) src, *d = (unsigned char *) dest;
         if (len % 32)
                 return -1;
-        run_ec(OP_ENCODE, len, 1, 1, 0, gftbl, &s, 1, &d);
+        run_ec("gf_vect_mul", OP_ENCODE, len, 1, 1, 0, gftbl, &s, 1, &d);
         return 0;
 }
 
@@ -1781,6 +1977,35 @@ int
 gf_vect_mul_base(int len, unsigned char *gftbl, unsigned char *src, unsigned char *dest)
 {
         return gf_vect_mul(len, gftbl, src, dest);
+}
+
+/* ---- device of an object's calls ------------------------------------------ */
+
+/* Make dev the calling thread's current device for one call on an object that
+ * belongs to it (a batch, a pipeline). Returns the device to restore with
+ * isal_hip_dev_leave (-1: no switch was needed), or -2 when the switch failed. */
+int
+isal_hip_dev_enter(int dev)
+{
+        int cur;
+        if (hipGetDevice(&cur) != hipSuccess) {
+                (void) hipGetLastError();
+                return -1;
+        }
+        if (cur == dev)
+                return -1;
+        if (hipSetDevice(dev) != hipSuccess) {
+                (void) hipGetLastError();
+                return -2;
+        }
+        return cur;
+}
+
+void
+isal_hip_dev_leave(int prev)
+{
+        if (prev >= 0)
+                (void) hipSetDevice(prev);
 }
 
 /* ---- batched extension (isal_hip.h) ------------------------------------ */
@@ -1801,6 +2026,50 @@ struct isal_hip_batch {
         int c64_tt;
         uint64_t *d_c64tab[ISAL_HIP_CRC64_NVARIANTS], *d_c64part;
 };
+
+/* Every shard of a batch on device dev: hipMalloc memory of dev, managed
+ * memory, or page-locked host memory whose device address is its host address.
+ * A stripe's shards usually come from a few allocations, so a device range
+ * already seen answers without a HIP query. */
+static int
+batch_check_ptrs(const uint64_t *ptrs, size_t n, size_t len, int dev)
+{
+        seen_t sn;
+        size_t i;
+        sn.n = 0;
+        for (i = 0; i < n; i++) {
+                const void *p = (const void *) (uintptr_t) ptrs[i];
+                hipPointerAttribute_t a;
+                int sd;
+                if (!p)
+                        return ISAL_HIP_EINVAL;
+                if ((sd = seen_dev(&sn, p, len)) >= 0) {
+                        if (sd != dev)
+                                return ISAL_HIP_EDEVICE;
+                        continue;
+                }
+                if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+                        (void) hipGetLastError();
+                        return ISAL_HIP_EINVAL; /* pageable: no kernel can reach it */
+                }
+                if (a.type == hipMemoryTypeDevice) {
+                        hipDeviceptr_t base;
+                        size_t size;
+                        if (a.device != dev)
+                                return ISAL_HIP_EDEVICE;
+                        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t) p) == hipSuccess)
+                                seen_add(&sn, (uintptr_t) base, size, a.device);
+                        else
+                                (void) hipGetLastError();
+                } else if (a.type == hipMemoryTypeHost) {
+                        if (a.devicePointer != p)
+                                return ISAL_HIP_EINVAL;
+                } else if (a.type != hipMemoryTypeManaged && a.type != hipMemoryTypeUnified) {
+                        return ISAL_HIP_EINVAL;
+                }
+        }
+        return ISAL_HIP_OK;
+}
 
 int
 isal_hip_batch_create(isal_hip_batch **out, int len, int k, int rows, const unsigned char *gftbls,
@@ -1837,8 +2106,17 @@ isal_hip_batch_create(isal_hip_batch **out, int len, int k, int rows, const unsi
         b->rows = rows;
         b->nstripes = nstripes;
         b->vec16 = vec16;
-        if (hipGetDevice(&b->device) != hipSuccess ||
-            hipMalloc((void **) &b->d_ptrs, nptr * 8) != hipSuccess ||
+        if (hipGetDevice(&b->device) != hipSuccess) {
+                free(h_ptrs);
+                isal_hip_batch_destroy(b);
+                return ISAL_HIP_EHIP;
+        }
+        if (len > 0 && (j = batch_check_ptrs(h_ptrs, nptr, (size_t) len, b->device)) != ISAL_HIP_OK) {
+                free(h_ptrs);
+                isal_hip_batch_destroy(b);
+                return j;
+        }
+        if (hipMalloc((void **) &b->d_ptrs, nptr * 8) != hipSuccess ||
             hipMemcpy(b->d_ptrs, h_ptrs, nptr * 8, hipMemcpyHostToDevice) != hipSuccess) {
                 free(h_ptrs);
                 isal_hip_batch_destroy(b);
@@ -1853,8 +2131,8 @@ isal_hip_batch_create(isal_hip_batch **out, int len, int k, int rows, const unsi
         return ISAL_HIP_OK;
 }
 
-int
-isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
+static int
+batch_set_tables_impl(isal_hip_batch *b, const unsigned char *gftbls)
 {
         size_t n;
         uint32_t *h;
@@ -1893,8 +2171,8 @@ isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
         return ISAL_HIP_OK;
 }
 
-int
-isal_hip_batch_encode(isal_hip_batch *b, void *stream)
+static int
+batch_encode_impl(isal_hip_batch *b, void *stream)
 {
         if (!b)
                 return ISAL_HIP_EINVAL;
@@ -1904,8 +2182,8 @@ isal_hip_batch_encode(isal_hip_batch *b, void *stream)
                        : ISAL_HIP_OK;
 }
 
-int
-isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream)
+static int
+batch_update_impl(isal_hip_batch *b, int vec_i, void *stream)
 {
         if (!b || vec_i < 0 || vec_i >= b->k)
                 return ISAL_HIP_EINVAL;
@@ -1915,8 +2193,8 @@ isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream)
                        : ISAL_HIP_OK;
 }
 
-int
-isal_hip_batch_check(isal_hip_batch *b, unsigned long long *bad, void *stream)
+static int
+batch_check_impl(isal_hip_batch *b, unsigned long long *bad, void *stream)
 {
         if (!b || !bad || !b->vec16)
                 return ISAL_HIP_EINVAL;
@@ -2034,8 +2312,8 @@ batch_crc_empty(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *s
                        : ISAL_HIP_EHIP;
 }
 
-int
-isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+static int
+batch_crc_impl(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
 {
         int r;
         if (!b || !crc)
@@ -2098,8 +2376,8 @@ batch_crc64_setup(isal_hip_batch *b, int variant)
         return ISAL_HIP_OK;
 }
 
-int
-isal_hip_batch_crc64(isal_hip_batch *b, int variant, unsigned long long init,
+static int
+batch_crc64_impl(isal_hip_batch *b, int variant, unsigned long long init,
                      unsigned long long *crc, void *stream)
 {
         int r;
@@ -2116,8 +2394,8 @@ isal_hip_batch_crc64(isal_hip_batch *b, int variant, unsigned long long init,
                        : ISAL_HIP_OK;
 }
 
-int
-isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long init,
+static int
+batch_encode_crc64_impl(isal_hip_batch *b, int variant, unsigned long long init,
                             unsigned long long *crc, void *stream)
 {
         int r;
@@ -2143,8 +2421,8 @@ isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long i
         return isal_hip_batch_crc64(b, variant, init, crc, stream);
 }
 
-int
-isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+static int
+batch_encode_crc_impl(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
 {
         int r;
         if (!b || !crc)
@@ -2170,4 +2448,112 @@ isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *cr
                         return ISAL_HIP_EHIP;
         }
         return batch_crc_finish(b, init, crc, stream);
+}
+
+/* ---- the batch entry points run on the batch's device -------------------- */
+
+int
+isal_hip_batch_set_tables(isal_hip_batch *b, const unsigned char *gftbls)
+{
+        int prev, r;
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(b->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = batch_set_tables_impl(b, gftbls);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+int
+isal_hip_batch_encode(isal_hip_batch *b, void *stream)
+{
+        int prev, r;
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(b->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = batch_encode_impl(b, stream);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+int
+isal_hip_batch_update(isal_hip_batch *b, int vec_i, void *stream)
+{
+        int prev, r;
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(b->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = batch_update_impl(b, vec_i, stream);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+int
+isal_hip_batch_check(isal_hip_batch *b, unsigned long long *bad, void *stream)
+{
+        int prev, r;
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(b->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = batch_check_impl(b, bad, stream);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+int
+isal_hip_batch_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+{
+        int prev, r;
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(b->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = batch_crc_impl(b, init, crc, stream);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+int
+isal_hip_batch_crc64(isal_hip_batch *b, int variant, unsigned long long init,
+                     unsigned long long *crc, void *stream)
+{
+        int prev, r;
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(b->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = batch_crc64_impl(b, variant, init, crc, stream);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+int
+isal_hip_batch_encode_crc64(isal_hip_batch *b, int variant, unsigned long long init,
+                            unsigned long long *crc, void *stream)
+{
+        int prev, r;
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(b->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = batch_encode_crc64_impl(b, variant, init, crc, stream);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+int
+isal_hip_batch_encode_crc(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *stream)
+{
+        int prev, r;
+        if (!b)
+                return ISAL_HIP_EINVAL;
+        if ((prev = isal_hip_dev_enter(b->device)) == -2)
+                return ISAL_HIP_EHIP;
+        r = batch_encode_crc_impl(b, init, crc, stream);
+        isal_hip_dev_leave(prev);
+        return r;
 }

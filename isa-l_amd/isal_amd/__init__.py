@@ -28,6 +28,7 @@ __all__ = [
     "gf_vect_dot_prod", "gf_vect_dot_prod_base", "gf_vect_mad", "gf_vect_mad_base",
     "gf_vect_mul", "gf_vect_mul_base", "Batch", "Pipe", "kernel_launches", "max_rows_per_pass",
     "version", "addr", "cpu_calls", "fallbacks", "reload_config", "Multi", "partition",
+    "route_device", "contexts_created", "selftest_kernels",
 ]
 
 LIB_PATH = os.environ.get(
@@ -124,6 +125,10 @@ def lib() -> ctypes.CDLL:
             "isal_hip_config_reload": (None, []),
             "isal_hip_max_rows_per_pass": (i, []),
             "isal_hip_target": (ctypes.c_char_p, []),
+            "isal_hip_route_device": (i, [i, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), i,
+                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+            "isal_hip_contexts_created": (ctypes.c_ulonglong, []),
+            "isal_hip_selftest_kernels": (i, [ctypes.POINTER(ctypes.c_int)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -458,6 +463,34 @@ def numa_node_cpus(node: int, sysfs_root: str | None = None) -> list[int] | None
     buf = (ctypes.c_int * 4096)()
     n = lib().isal_hip_numa_node_cpus(sysfs_root.encode() if sysfs_root else None, node, buf, 4096)
     return None if n < 0 else list(buf[:min(n, 4096)])
+
+
+MEM_PAGEABLE, MEM_DEVICE, MEM_MANAGED, MEM_PINNED = 0, 1, 2, 3
+
+
+def route_device(kinds: Sequence[int], devs: Sequence[int], cur: int) -> tuple[int, int, list[int]]:
+    """isal_hip_route_device: the device a drop-in call with these shards runs
+    on (-2: device shards on two GPUs), the first shard on a second GPU (-1:
+    none) and the per-shard in-place flags. Pure logic, no GPU needed."""
+    n = len(kinds)
+    K = (ctypes.c_int * max(n, 1))(*kinds)
+    D = (ctypes.c_int * max(n, 1))(*devs)
+    P = (ctypes.c_int * max(n, 1))()
+    bad = ctypes.c_int(0)
+    dev = lib().isal_hip_route_device(n, K, D, cur, ctypes.byref(bad), P)
+    return dev, bad.value, list(P[:n])
+
+
+def selftest_kernels() -> tuple[int, int]:
+    """isal_hip_selftest_kernels: (kernels without usable device code, kernels checked)."""
+    n = ctypes.c_int(0)
+    bad = lib().isal_hip_selftest_kernels(ctypes.byref(n))
+    return int(bad), int(n.value)
+
+
+def contexts_created() -> int:
+    """Per-thread, per-device contexts the drop-in calls have created."""
+    return int(lib().isal_hip_contexts_created())
 
 
 def kernel_launches() -> int:

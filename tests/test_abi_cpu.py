@@ -159,3 +159,42 @@ def test_numa_lookup_against_a_faked_sysfs(engine, tmp_path):
     # the real tree of this host parses (node 0 exists on every Linux box with NUMA)
     if os.path.exists("/sys/devices/system/node/node0/cpulist"):
         assert engine.numa_node_cpus(0, None)
+
+
+def test_route_device_choice_with_fabricated_attributes(engine):
+    """The drop-in calls' device choice (isal_hip_route_device, isal_hip.h
+    "Several GPUs"): the reference API has no device argument
+    (erasure_code.h:108-110), so a call runs on the GPU holding its
+    device-resident shards. Driven here with fabricated pointer attributes:
+    host-only calls, a foreign device, two devices in one call, managed
+    memory, page-locked memory of the run device and of another one."""
+    PG, DV, MG, PN = engine.MEM_PAGEABLE, engine.MEM_DEVICE, engine.MEM_MANAGED, engine.MEM_PINNED
+    rd = engine.route_device
+    # host shards only: the caller's current device, nothing in place
+    assert rd([PG] * 6, [-1] * 6, 0) == (0, -1, [0] * 6)
+    assert rd([PG] * 3, [-1] * 3, 5) == (5, -1, [0] * 3)
+    # device shards on a GPU other than the current one: that GPU
+    assert rd([DV] * 4 + [PG], [3] * 4 + [-1], 0) == (3, -1, [1, 1, 1, 1, 0])
+    assert rd([PG, DV, PG], [-1, 7, -1], 2) == (7, -1, [0, 1, 0])
+    # device shards on two GPUs: refused, naming the first shard on the second
+    dev, bad, _ = rd([DV, DV, DV, DV], [2, 2, 5, 2], 2)
+    assert (dev, bad) == (-2, 2)
+    dev, bad, _ = rd([PG, DV, MG, DV], [-1, 1, -1, 0], 0)
+    assert (dev, bad) == (-2, 3)
+    # managed memory binds no device and is used in place on any
+    assert rd([MG, DV, MG], [-1, 4, -1], 1) == (4, -1, [1, 1, 1])
+    assert rd([MG, MG], [-1, -1], 6) == (6, -1, [1, 1])
+    # page-locked memory: in place only on the GPU it was registered with
+    assert rd([PN, DV, PN], [0, 2, 2], 0) == (2, -1, [0, 1, 1])
+    assert rd([PN, PN], [1, 0], 0) == (0, -1, [0, 1])
+    # the caller's device unknown and no device shard: no device
+    assert rd([PG, PN], [-1, 0], -1) == (-1, -1, [0, 0])
+    # no shards; bad arguments
+    assert rd([], [], 3)[0] == 3
+    L = engine.lib()
+    assert L.isal_hip_route_device(-1, None, None, 0, None, None) == -3
+    assert L.isal_hip_route_device(2, None, None, 0, None, None) == -3
+    # a 64-shard stripe spread over 8 GPUs: the first foreign shard is reported
+    kinds, devs = [DV] * 64, [i // 8 for i in range(64)]
+    assert rd(kinds, devs, 0)[:2] == (-2, 8)
+

@@ -509,12 +509,14 @@ def test_dropin_kernel_args_vs_oracle(engine, oracle, gpu, monkeypatch, capfd, n
         assert np.array_equal(out[base + n: base + stride], canary[l * stride + n: (l + 1) * stride]), l
 
 
-def test_device_resident_failure_aborts_naming_the_call(gpu):
+@pytest.mark.parametrize("site,step", [("1", "ensure_done"), ("3", "encode launch (kernel arguments)")])
+def test_device_resident_failure_aborts_naming_the_call(gpu, site, step):
     """DESIGN §2 'Failures': a call with device-resident shards cannot fall back
     to the CPU route, so a failing HIP step aborts the process with the step
     named. A child process makes one kernel-argument call with a fault
-    injected at the allocation site (ISAL_HIP_FAULT=1: before any launch, so
-    no GPU work is in flight when it aborts)."""
+    injected at the allocation site (ISAL_HIP_FAULT=1) or at the launch
+    (=3): both fire before anything is launched, so no GPU work is in flight
+    when it aborts."""
     code = (
         "import sys; sys.path.insert(0, 'isa-l_amd'); import torch, isal_amd as e\n"
         "k, r, n = 4, 2, 65536\n"
@@ -523,11 +525,11 @@ def test_device_resident_failure_aborts_naming_the_call(gpu):
         "e.ec_encode_data(n, k, r, t, [b[j] for j in range(k)], [b[k + l] for l in range(r)])\n"
         "print('returned')\n")
     env = {x: v for x, v in os.environ.items() if not x.startswith("ISAL_HIP_")}
-    env["ISAL_HIP_FAULT"] = "1"
+    env["ISAL_HIP_FAULT"] = site
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=ecutil.REPO,
                        timeout=300)
     assert p.returncode != 0 and "returned" not in p.stdout, (p.returncode, p.stdout, p.stderr[-2000:])
-    assert "ensure_done" in p.stderr and "device-resident shards" in p.stderr and "aborting" in p.stderr, \
+    assert step in p.stderr and "device-resident shards" in p.stderr and "aborting" in p.stderr, \
         p.stderr[-2000:]
 
 
@@ -1930,29 +1932,38 @@ def test_dropin_result_visible_to_other_streams(engine, oracle, gpu):
     written the host mailbox (isal_hip_kdone), before the runtime has seen the
     kernel end: the parity must already be visible to work the caller issues
     right away on a NON-blocking stream (no implicit ordering with the
-    engine's stream) — a copy to the host and a kernel reading it."""
+    engine's stream, no synchronize in between) — a copy to the host and a
+    kernel reading it. Encode and update, at a 16-byte multiple and at a ragged
+    length (whose per-byte tail takes the one agent-scope writeback)."""
     import torch
 
-    k, rows, n = 10, 4, 256 << 10
+    k, rows = 10, 4
     coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
     tbls = engine.ec_init_tables(k, rows, coef)
-    src = torch.empty((k, n), dtype=torch.uint8, device=gpu)
-    out = torch.zeros((rows, n), dtype=torch.uint8, device=gpu)
-    side = torch.cuda.Stream(device=gpu)
-    pin = torch.empty((rows, n), dtype=torch.uint8).pin_memory()
-    for it in range(24):
-        src.random_(generator=torch.Generator(device=gpu).manual_seed(100 + it))
-        torch.cuda.synchronize()
-        engine.ec_encode_data(n, k, rows, tbls, [src[j] for j in range(k)], [out[l] for l in range(rows)])
-        with torch.cuda.stream(side):
-            pin.copy_(out, non_blocking=True)
-            x = out[0].clone()  # a kernel on the side stream reading row 0
-        side.synchronize()
-        h = _host(src)
-        want = oracle.encode(coef, k, rows, [h[j] for j in range(k)])
-        for l in range(rows):
-            assert np.array_equal(pin[l].numpy(), want[l]), (it, l)
-        assert np.array_equal(_host(x), want[0]), it
+    side = torch.cuda.Stream(device=gpu)  # torch creates it non-blocking
+    for n in (256 << 10, (256 << 10) + 5, 4096 * 3 + 13):
+        src = torch.empty((k, n), dtype=torch.uint8, device=gpu)
+        out = torch.zeros((rows, n), dtype=torch.uint8, device=gpu)
+        pin = torch.empty((rows, n), dtype=torch.uint8).pin_memory()
+        for it in range(12):
+            src.random_(generator=torch.Generator(device=gpu).manual_seed(100 + it + n))
+            h = _host(src)
+            want = oracle.encode(coef, k, rows, [h[j] for j in range(k)])
+            torch.cuda.synchronize()
+            if it % 2 == 0:
+                engine.ec_encode_data(n, k, rows, tbls, [src[j] for j in range(k)], [out[l] for l in range(rows)])
+            else:
+                out.zero_()
+                torch.cuda.synchronize()
+                for v in range(k):
+                    engine.ec_encode_data_update(n, k, rows, v, tbls, src[v], [out[l] for l in range(rows)])
+            with torch.cuda.stream(side):
+                pin.copy_(out, non_blocking=True)
+                x = out[rows - 1].clone()  # a kernel on the side stream reading the last row
+            side.synchronize()
+            for l in range(rows):
+                assert np.array_equal(pin[l].numpy(), want[l]), (n, it, l)
+            assert np.array_equal(_host(x), want[rows - 1]), (n, it)
 
 
 @pytest.mark.parametrize("done", ["1", "0"])
@@ -2150,3 +2161,93 @@ def test_batch_check_vs_oracle(engine, oracle, gpu, monkeypatch, xor, k, rows, n
         row = int(np.nonzero(mism[:, col])[0][0])
         assert int(got[s]) == (col << 8) | row, (s, flips.get(s), hex(int(got[s])), col, row)
     b.close()
+
+
+def test_one_context_per_thread_and_device(engine, oracle, gpu):
+    """A thread keeps one context (stream, buffers, mailbox) per GPU it calls
+    on: 1,000 drop-in calls from a fresh thread that calls hipSetDevice(0)
+    between them create exactly one (isal_hip_contexts_created), every result
+    matches the oracle, and the thread's current device is unchanged after
+    each call (isal_hip.h "Several GPUs")."""
+    import ctypes
+
+    import torch
+
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already holds (same SONAME)
+    dev = torch.device(gpu).index or 0
+    k, rows, n = 10, 4, 64 << 10
+    coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+    tbls = engine.ec_init_tables(k, rows, coef)
+    src = torch.empty((k, n), dtype=torch.uint8, device=gpu).random_(generator=torch.Generator(device=gpu).manual_seed(9))
+    h = _host(src)
+    want = oracle.encode(coef, k, rows, [h[j] for j in range(k)])
+    res = {}
+
+    def worker():
+        try:
+            out = torch.zeros((rows, n), dtype=torch.uint8, device=gpu)
+            torch.cuda.synchronize()
+            before = engine.contexts_created()
+            cur = ctypes.c_int(-1)
+            moved = 0
+            for it in range(1000):
+                assert hip.hipSetDevice(dev) == 0
+                engine.ec_encode_data(n, k, rows, tbls, [src[j] for j in range(k)], [out[l] for l in range(rows)])
+                hip.hipGetDevice(ctypes.byref(cur))
+                moved += cur.value != dev
+            res["delta"] = engine.contexts_created() - before
+            res["moved"] = moved
+            res["ok"] = all(np.array_equal(_host(out[l]), want[l]) for l in range(rows))
+        except Exception as e:  # pragma: no cover - reported below
+            res["err"] = repr(e)
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join()
+    assert "err" not in res, res
+    assert res["delta"] == 1, res
+    assert res["moved"] == 0 and res["ok"], res
+
+
+def test_batch_rejects_memory_no_kernel_of_its_device_can_reach(engine, gpu):
+    """isal_hip_batch_create accepts only shards its device's kernels reach:
+    hipMalloc memory of its device (and managed / page-locked host memory);
+    pageable host memory is ISAL_HIP_EINVAL, checked before anything is
+    allocated (memory of another GPU, ISAL_HIP_EDEVICE, needs a second GPU)."""
+    import ctypes
+
+    import torch
+
+    L = engine.lib()
+    k, rows, n, ns = 4, 2, 4096, 3
+    tbls = engine.ec_init_tables(k, rows, engine.gf_gen_rs_matrix(k + rows, k)[k * k:])
+    dev = torch.zeros((ns * (k + rows), n), dtype=torch.uint8, device=gpu)
+    pinned = torch.zeros((ns * (k + rows), n), dtype=torch.uint8).pin_memory()
+    pageable = np.zeros((ns * (k + rows), n), np.uint8)
+    u8p = ctypes.POINTER(ctypes.c_ubyte)
+
+    def create(rows_of):
+        data = (u8p * (ns * k))(*[ctypes.cast(rows_of(s * (k + rows) + j), u8p) for s in range(ns) for j in range(k)])
+        coding = (u8p * (ns * rows))(*[ctypes.cast(rows_of(s * (k + rows) + k + l), u8p)
+                                       for s in range(ns) for l in range(rows)])
+        h = ctypes.c_void_p()
+        rc = L.isal_hip_batch_create(ctypes.byref(h), n, k, rows, ctypes.cast(tbls.ctypes.data, u8p), ns, data, coding)
+        if rc == 0:
+            L.isal_hip_batch_destroy(h)
+        return rc
+
+    assert create(lambda i: dev[i].data_ptr()) == 0
+    assert create(lambda i: pinned[i].data_ptr()) == 0
+    assert create(lambda i: pageable[i].ctypes.data) == -1
+    # one pageable shard among device ones
+    assert create(lambda i: pageable[i].ctypes.data if i == 7 else dev[i].data_ptr()) == -1
+
+
+def test_selftest_every_launchable_kernel_resolves(engine, gpu):
+    """isal_hip_selftest_kernels: the HIP runtime resolves every kernel the
+    launchers can select (encode, LDS-DMA, verify, update, kernel-argument,
+    CRC32C, CRC64, fused) — a missing one is a test failure here instead of
+    an abort in a caller's launch (DESIGN.md §3 "Kernel registry")."""
+    bad, n = engine.selftest_kernels()
+    assert n > 800, n
+    assert bad == 0, f"{bad} of {n} kernels have no usable device code (named on stderr)"

@@ -4,6 +4,11 @@
 #   steps: tests bench crc prof pmc decode update e2e probe
 # Every GPU step runs under its own timeout and the chain stops at the first
 # failure; outputs land in gpurun_out/TAG/.
+# Round 6 pruned the A/B steps whose variant knobs round 5 removed (their
+# arms would now run the same kernel): hybrid pipe64 pipe32 prepipe pre8 order
+# xcd encstore occ ldsmin updocc c2ab grid dropinspin crc64step slice64 fastcrc
+# crcp prestand encrc64sweep crcstep. Their results stay in profiles/ and
+# DESIGN.md §2b; tools/gpu_runs/ keeps the commands as they were run.
 set -o pipefail
 TAG=${1:-run}
 shift
@@ -46,86 +51,6 @@ for s in $STEPS; do
         faulttests)
                 run pytest_gpu_fault 600 python -u -m pytest tests -m gpu -x -v -k "hip_failure or large_host_call or multi_device or pinned_host" --timeout 300 --timeout-method thread
                 ;;
-        hybrid)
-                # fused encode+CRC64: byte tables (1) vs hybrid byte/field tables (2), LDS counters of each
-                run pytest_gpu_hybrid 900 python -u -m pytest tests -m gpu -x -v -k "encode_crc64_slice_knobs or encode_crc64_every_flavour" --timeout 300 --timeout-method thread
-                for r in 1 2; do
-                        for sl in 1 2; do
-                                ISAL_HIP_CRC64_SLICE=$sl run bench_encrc64_sl${sl}_r$r 300 python bench.py --workload encode-crc64 --no-cpu-baseline
-                        done
-                done
-                for sl in 1 2; do
-                        ISAL_HIP_CRC64_SLICE=$sl run pmc_lds_encrc64_sl$sl 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_encrc64_sl$sl" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
-                        ISAL_HIP_CRC64_SLICE=$sl run rocprof_encrc64_sl$sl 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_encrc64_sl$sl" -o e -- python3 bench.py --workload encode-crc64 --no-cpu-baseline
-                done
-                ;;
-        pipe64)
-                # fused encode+CRC64: byte tables (SL 1) vs chain steps pipelined into the GF rows (SL 3)
-                run pytest_gpu_pipe64 600 python -u -m pytest tests -m gpu -x -v -k "crc64_pipelined or encode_crc64_every_flavour or encode_crc64_slice_knobs" --timeout 300 --timeout-method thread
-                for r in 1 2; do
-                        for cfg in ${PIPE64_CFGS:-1:0 3:1 3:2}; do
-                                ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run bench_encrc64_sl${cfg/:/_nv}_r$r 300 python bench.py --workload encode-crc64 --no-cpu-baseline
-                        done
-                done
-                for cfg in ${PIPE64_PMC:-1:0 3:1}; do
-                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run pmc_lds_sl${cfg/:/_nv} 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_sl${cfg/:/_nv}" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
-                done
-                ;;
-        pipe32)
-                # fused encode+CRC32C: byte tables (NB 4) vs chain steps pipelined into the GF rows (NB 8)
-                run pytest_gpu_pipe32 600 python -u -m pytest tests -m gpu -x -v -k "crc_pipelined or encode_crc_byte_tables or crc64_pipelined" --timeout 300 --timeout-method thread
-                for r in 1 2; do
-                        for cfg in ${PIPE32_CFGS:-4:0 8:1 8:2}; do
-                                ISAL_HIP_CRC_BYTE_DWORDS=${cfg%:*} ISAL_HIP_CRC_FUSED_NV=${cfg#*:} run bench_encrc_nb${cfg/:/_nv}_r$r 300 python bench.py --workload encode-crc --no-cpu-baseline
-                        done
-                        run bench_encrc64_r$r 300 python bench.py --workload encode-crc64 --no-cpu-baseline
-                done
-                ;;
-        prepipe)
-                # checksum-only CRC64: pre-shifted kernel with pipelined lookups (1, default) vs not (0)
-                run pytest_gpu_crc64 400 python -u -m pytest tests -m gpu -x -v -k "crc64 and not encode" --timeout 200 --timeout-method thread
-                for r in 1 2; do
-                        for pp in 0 1; do
-                                for b in ${PP_BATCHES:-4}; do
-                                        ISAL_HIP_CRC64_PRE_PIPE=$pp ISAL_HIP_CRC64_BATCH=$b run bench_crc64_pp${pp}_b${b}_r$r 300 python bench.py --workload crc64 --no-cpu-baseline
-                                done
-                        done
-                done
-                for pp in 0 1; do
-                        ISAL_HIP_CRC64_PRE_PIPE=$pp run pmc_lds_crc64_pp$pp 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_crc64_pp$pp" -o l -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 2 --warmup 1
-                done
-                run rocprof_crc64 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_crc64" -o crc64 -- python3 bench.py --workload crc64 --no-cpu-baseline
-                ;;
-        pre8)
-                # checksum-only CRC64: pre-shifted kernel with 4 or 8 tiles per load batch
-                for r in 1 2; do
-                        for b in 4 8; do
-                                ISAL_HIP_CRC64_BATCH=$b run bench_crc64_b${b}_r$r 300 python bench.py --workload crc64 --no-cpu-baseline
-                        done
-                done
-                ;;
-        order)
-                # encode work order: tile-fastest (0) vs XCD-contiguous (2), interleaved
-                run pytest_gpu_order 300 python -u -m pytest tests -m gpu -x -v -k "xcd_order" --timeout 200 --timeout-method thread
-                for r in 1 2 3; do
-                        for o in 0 2; do
-                                ISAL_HIP_ENC_ORDER=$o run bench_c2_order${o}_r$r 300 python bench.py --no-cpu-baseline
-                        done
-                done
-                rocm-smi --showbus > "$OUT/bus.txt" 2>&1 || true
-                ;;
-        xcd)
-                # update / CRC kernels: tile-fastest items vs XCD-contiguous items (ISAL_HIP_XCD_ORDER)
-                run pytest_gpu_xcd 300 python -u -m pytest tests -m gpu -x -v -k "xcd" --timeout 200 --timeout-method thread
-                for r in 1 2; do
-                        for o in 0 1; do
-                                for wl in "update --k 20 --p 6 --len 4194304 --stripes 64" "crc" "crc64" "encode-crc" "encode-crc64"; do
-                                        tag=$(echo $wl | cut -d' ' -f1)
-                                        ISAL_HIP_XCD_ORDER=$o run bench_${tag}_x${o}_r$r 300 python bench.py --workload $wl --no-cpu-baseline
-                                done
-                        done
-                done
-                ;;
         fuzzgpu)
                 # differential fuzzing of the shipped library on the kernels (tests/fuzz)
                 python3 tests/fuzz/seeds.py diff "$OUT/fuzz_corpus" > /dev/null
@@ -135,15 +60,6 @@ for s in $STEPS; do
         gpus2)
                 # the driver's N>1 form on this one-GPU box: two gloo ranks share the GPU
                 run bench_gpus2_gloo 300 python bench.py --gpus 2 --dist-backend gloo --no-cpu-baseline
-                ;;
-        encstore)
-                # encode parity stores: nt (0, default) vs sc1 + nt (1), interleaved
-                run pytest_gpu_encstore 300 python -u -m pytest tests -m gpu -x -v -k "xcd_order_vs_oracle" --timeout 200 --timeout-method thread
-                for r in 1 2 3; do
-                        for st in 0 1; do
-                                ISAL_HIP_ENC_STORE=$st run bench_c2_store${st}_r$r 300 python bench.py --no-cpu-baseline
-                        done
-                done
                 ;;
         gpus8)
                 # rehearsal of the driver's N=8 launch forms on this one-GPU box: eight gloo
@@ -264,35 +180,6 @@ for s in $STEPS; do
         labels)
                 run pytest_gpu_labels 900 python -u -m pytest tests -m gpu -x -v -k "kernel_label or dropin_kernel_args or smoke" --timeout 300 --timeout-method thread
                 ;;
-        occ)
-                # occupancy cap through unused LDS per workgroup (ISAL_HIP_ENC_LDS_PAD)
-                for r in 1 2; do
-                        for pad in 0 22528 27136 32768 40960; do
-                                ISAL_HIP_ENC_LDS_MIN=$pad run bench_c2_pad${pad}_r$r 300 python bench.py --no-cpu-baseline
-                                ISAL_HIP_ENC_LDS_MIN=$pad run bench_decode_pad${pad}_r$r 300 python bench.py --workload decode --no-cpu-baseline
-                        done
-                done
-                ;;
-        ldsmin)
-                # encode occupancy cap (ISAL_HIP_ENC_LDS_MIN, default 32 KiB) vs none, per shape
-                run pytest_gpu_ldsmin 600 python -u -m pytest tests -m gpu -x -q -k "xor_fast_path or load_groups or random_shapes or decode or raid or golden" --timeout 300 --timeout-method thread
-                for r in 1 2; do
-                        for w in "encode --k 10 --p 4" "decode" "encode --k 10 --p 1" "encode --k 10 --p 2" "encode --k 10 --p 6" "encode --k 10 --p 8" "encode --k 20 --p 6 --len 4194304 --stripes 64" "encode --k 4 --p 2"; do
-                                tag=$(echo $w | tr -d ' -' | cut -c1-24)
-                                for m in 0 32768; do
-                                        ISAL_HIP_ENC_LDS_MIN=$m run bench_${tag}_m${m}_r$r 300 python bench.py --workload $w --no-cpu-baseline
-                                done
-                        done
-                done
-                ;;
-        updocc)
-                # update kernel occupancy cap (ISAL_HIP_UPD_LDS_MIN)
-                for r in 1 2; do
-                        for m in 0 22528 27136 32768 40960; do
-                                ISAL_HIP_UPD_LDS_MIN=$m run bench_update_m${m}_r$r 300 python bench.py --workload update --k 20 --p 6 --len 4194304 --stripes 64 --no-cpu-baseline
-                        done
-                done
-                ;;
         confirm)
                 run pytest_gpu_confirm 600 python -u -m pytest tests -m gpu -x -q -k "xor_fast_path or load_groups or random_shapes or decode or raid or golden or kernel_label or smoke" --timeout 300 --timeout-method thread
                 for w in "encode" "decode" "encode --k 20 --p 6 --len 4194304 --stripes 64" "encode --k 10 --p 2" "encode --k 10 --p 8"; do
@@ -300,26 +187,8 @@ for s in $STEPS; do
                         run bench_${tag}_default 300 python bench.py --workload $w --no-cpu-baseline
                 done
                 ;;
-        c2ab)
-                # C2 and C3 with the narrow-pass occupancy cap (default) and without
-                for r in 1 2 3; do
-                        for m in d 0; do
-                                v=$m; [ "$m" = d ] && v=
-                                ISAL_HIP_ENC_LDS_MIN=$v run bench_c2_m${m}_r$r 300 python bench.py --no-cpu-baseline
-                                ISAL_HIP_ENC_LDS_MIN=$v run bench_decode_m${m}_r$r 300 python bench.py --workload decode --no-cpu-baseline
-                        done
-                done
-                ;;
         ldsinfo)
                 run lds_info 60 python3 -c "import torch, ctypes; torch.zeros(1, device='cuda'); l = ctypes.CDLL('tools/libcopy_probe.so'); print('lds_per_cu', l.copy_probe_lds_per_cu()); [print('dyn', d, 'blocks_per_cu', l.copy_probe_blocks_per_cu(ctypes.c_ulonglong(d))) for d in (0, 16384, 22528, 27136, 32768, 40960, 65536)]"
-                ;;
-        grid)
-                # grid-stride launches of at most n workgroups (ISAL_HIP_GRID_CAP)
-                for r in 1 2; do
-                        for cap in 0 2048 4096 8192 16384; do
-                                ISAL_HIP_GRID_CAP=$cap run bench_c2_cap${cap}_r$r 300 python bench.py --no-cpu-baseline
-                        done
-                done
                 ;;
         fuzzrss)
                 # the GPU differential fuzz target for 150 s with libFuzzer's 2 GiB RSS /
@@ -340,10 +209,6 @@ for s in $STEPS; do
                                 ISAL_HIP_ENC_LDS=$x run pmc_sq_k$1p$2_lds$x 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_k$1p$2_lds$x" -o s -- python3 bench.py --workload encode --k $1 --p $2 --len $3 --stripes $4 --no-cpu-baseline --steps 2 --warmup 1
                         done
                 done
-                ;;
-        dropinspin)
-                run bench_dropin_block 300 python bench.py --workload dropin
-                ISAL_HIP_SYNC_SPIN=1 run bench_dropin_spin 300 python bench.py --workload dropin
                 ;;
         dropintests)
                 run pytest_gpu_dropin 600 python -u -m pytest tests -m gpu -x -v -k "dropin or concurrent or pinned or golden or device or xor_fast_path or smoke or raid" --timeout 300 --timeout-method thread
@@ -386,64 +251,6 @@ for s in $STEPS; do
                 run pmc_write_encrc64 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_encrc64" -o w -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 3 --warmup 1
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_encode_crc64.csv" "workload=encode-crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode-crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encrc64" "$OUT/pmc_write_encrc64" ec_encode_crc64_v16
                 ;;
-        crc64step)
-                run pytest_gpu_crc64 300 python -u -m pytest tests -m gpu -x -v -k "crc64" --timeout 200 --timeout-method thread
-                for mb in 1:4 2:4 4:4 1:8 2:8 4:8; do
-                        ISAL_HIP_CRC64_STEP=${mb%:*} ISAL_HIP_CRC64_BATCH=${mb#*:} run bench_crc64_step${mb/:/_b} 300 python bench.py --workload crc64 --no-cpu-baseline
-                done
-                run bench_crc64 300 python bench.py --workload crc64 --cpu-seconds 5
-                run rocprof_crc64 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_crc64" -o crc64 -- python3 bench.py --workload crc64 --no-cpu-baseline
-                run pmc_fetch_crc64 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_crc64" -o f -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 3 --warmup 1
-                run pmc_write_crc64 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_crc64" -o w -- python3 bench.py --workload crc64 --no-cpu-baseline --steps 3 --warmup 1
-                python3 tools/pmc_csv.py "$OUT/pmc_c2_crc64.csv" "workload=crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_crc64" "$OUT/pmc_write_crc64" crc64_shards
-                ;;
-        slice64)
-                # fused encode+CRC64: field tables vs slicing-by-8 chunk path, 1 or 2 lane groups per workgroup
-                run pytest_gpu_encrc64 500 python -u -m pytest tests -m gpu -x -v -k "encode_crc64" --timeout 200 --timeout-method thread
-                for cfg in ${SLICE64_CFGS:-0:1 0:2 1:1 1:2}; do
-                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run bench_encrc64_sl${cfg/:/_nv} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
-                done
-                for cfg in ${SLICE64_PMC:-1:2 0:2}; do
-                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run pmc_lds_sl${cfg/:/_nv} 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_sl${cfg/:/_nv}" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
-                done
-                ;;
-        fastcrc)
-                # byte-indexed CRC paths of the fused kernels: CRC32C byte tables, CRC64 slicing (+ lane groups)
-                run pytest_gpu_crc 700 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
-                for nb in 0 4; do
-                        ISAL_HIP_CRC_BYTE_DWORDS=$nb run bench_encrc_nb$nb 300 python bench.py --workload encode-crc --no-cpu-baseline
-                done
-                for cfg in ${SLICE64_CFGS:-0:1 0:2 1:1 1:2}; do
-                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run bench_encrc64_sl${cfg/:/_nv} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
-                done
-                ISAL_HIP_CRC_BYTE_DWORDS=4 run pmc_lds_encrc_nb4 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_encrc_nb4" -o l -- python3 bench.py --workload encode-crc --no-cpu-baseline --steps 2 --warmup 1
-                for cfg in ${SLICE64_PMC:-1:2 0:2}; do
-                        ISAL_HIP_CRC64_SLICE=${cfg%:*} ISAL_HIP_CRC64_FUSED_NV=${cfg#*:} run pmc_lds_sl${cfg/:/_nv} 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_sl${cfg/:/_nv}" -o l -- python3 bench.py --workload encode-crc64 --no-cpu-baseline --steps 2 --warmup 1
-                done
-                ;;
-        crcp)
-                # fast CRC paths vs field tables at fewer parity rows (less encode VALU to hide behind)
-                for p in 1 2; do
-                        for nb in 0 4; do
-                                ISAL_HIP_CRC_BYTE_DWORDS=$nb run bench_encrc_p${p}_nb$nb 300 python bench.py --workload encode-crc --p $p --no-cpu-baseline
-                        done
-                        for sl in 0 1; do
-                                ISAL_HIP_CRC64_SLICE=$sl run bench_encrc64_p${p}_sl$sl 300 python bench.py --workload encode-crc64 --p $p --no-cpu-baseline
-                        done
-                done
-                ;;
-        prestand)
-                # checksum-only kernels: pre-shifted chains vs chain-step kernels
-                run pytest_gpu_crc 700 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
-                for pre in 0 1; do
-                        for wl in crc crc64; do
-                                ISAL_HIP_CRC_PRE=$pre run bench_${wl}_pre$pre 300 python bench.py --workload $wl --no-cpu-baseline
-                        done
-                done
-                for wl in crc crc64; do
-                        run pmc_lds_${wl}_pre 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_lds_${wl}_pre" -o l -- python3 bench.py --workload $wl --no-cpu-baseline --steps 2 --warmup 1
-                done
-                ;;
         abprev)
                 # A/B against the previous build kept at isa-l_amd/lib/prev (same box)
                 run pytest_gpu_crc 700 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
@@ -482,18 +289,6 @@ for s in $STEPS; do
                 python3 tools/pmc_csv.py "$OUT/pmc_c2_encode_crc64.csv" "workload=encode-crc64 k=10 p=4 len=1048576 stripes=1024" "python bench.py --workload encode-crc64 --steps 3 --warmup 1 --no-cpu-baseline" "$OUT/pmc_fetch_encode-crc64" "$OUT/pmc_write_encode-crc64" ec_encode_crc64_v16
                 run bench_encode_crc 300 python bench.py --workload encode-crc --cpu-seconds 5
                 run bench_encode_crc64 300 python bench.py --workload encode-crc64 --cpu-seconds 5
-                ;;
-        encrc64sweep)
-                for cfg in ${ENCRC64_CFGS:-reg:10 lds:10 lds:5}; do
-                        ISAL_HIP_CRC64_SRC_CHAIN=${cfg%:*} ISAL_HIP_CRC64_FUSED_U=${cfg#*:} run bench_encrc64_${cfg/:/_u} 300 python bench.py --workload encode-crc64 --no-cpu-baseline
-                done
-                ;;
-        crcstep)
-                run pytest_gpu_crc 300 python -u -m pytest tests -m gpu -x -v -k "crc" --timeout 200 --timeout-method thread
-                for m in 1 4; do
-                        ISAL_HIP_CRC_STEP=$m run bench_crc_step$m 300 python bench.py --workload crc --no-cpu-baseline
-                done
-                run rocprof_crconly 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_crconly" -o crconly -- python3 bench.py --workload crc --no-cpu-baseline
                 ;;
         decode)
                 run bench_decode 300 python bench.py --workload decode --no-cpu-baseline
