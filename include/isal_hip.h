@@ -262,6 +262,11 @@ int isal_hip_route_device(int n, const int *kind, const int *dev, int cur, int *
  * process started (a thread's first call on each GPU makes one). */
 unsigned long long isal_hip_contexts_created(void);
 
+/* Kernel-argument drop-in calls whose completion word had not arrived after
+ * the 20 ms spin, so that hipStreamSynchronize completed them (the kernel
+ * waited behind other work, or ran long). */
+unsigned long long isal_hip_slow_waits(void);
+
 /* Drop-in calls served by the CPU route, and of those the HIP-failure
  * fallbacks, since the process started. */
 unsigned long long isal_hip_cpu_calls(void);

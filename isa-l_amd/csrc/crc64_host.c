@@ -22,6 +22,7 @@
  * so a wave's ds_read_b64 lookups into one table never bank-conflict.
  * Nothing here touches shard data.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -95,28 +96,76 @@ compose(const uint64_t a[64], const uint64_t b[64], uint64_t c[64])
                 c[i] = apply(a, b[i]);
 }
 
-/* Z^n as columns (square-and-multiply on Z^1). */
+/* Z^(2^i), i < ZP2_BITS, per flavour: built once per process (the drop-in
+ * checksum calls rebuild their length-dependent maps per length, which then
+ * costs one composition per set bit of the length, not a squaring chain). */
+#define ZP2_BITS 48
+#define NFLAVOURS 8 /* ISAL_HIP_CRC64_NVARIANTS */
+static uint64_t zp2[NFLAVOURS][ZP2_BITS][64];
+static int zp2_ready[NFLAVOURS];
+static pthread_mutex_t zp2_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static const uint64_t (*zpow2(int variant))[64]
+{
+        if (!__atomic_load_n(&zp2_ready[variant], __ATOMIC_ACQUIRE)) {
+                pthread_mutex_lock(&zp2_mu);
+                if (!zp2_ready[variant]) {
+                        int i, b;
+                        for (i = 0; i < 64; i++)
+                                zp2[variant][0][i] = raw_update(variant, 1ULL << i, NULL, 1);
+                        for (b = 1; b < ZP2_BITS; b++)
+                                compose(zp2[variant][b - 1], zp2[variant][b - 1], zp2[variant][b]);
+                        __atomic_store_n(&zp2_ready[variant], 1, __ATOMIC_RELEASE);
+                }
+                pthread_mutex_unlock(&zp2_mu);
+        }
+        return (const uint64_t (*)[64]) zp2[variant];
+}
+
+/* Z^n as columns (products of the cached Z^(2^i)). */
 void
 isal_hip_crc64_zpow(int variant, unsigned long long n, uint64_t out[64])
 {
-        uint64_t sq[64], acc[64], t[64];
-        int i;
-        for (i = 0; i < 64; i++) {
-                sq[i] = raw_update(variant, 1ULL << i, NULL, 1);
+        const uint64_t (*p2)[64] = zpow2(variant);
+        uint64_t acc[64], t[64];
+        int i, b;
+        for (i = 0; i < 64; i++)
                 acc[i] = 1ULL << i;
-        }
-        while (n) {
-                if (n & 1) {
+        for (b = 0; n; b++, n >>= 1) {
+                if (!(n & 1))
+                        continue;
+                if (b < ZP2_BITS) {
+                        compose(p2[b], acc, t);
+                } else { /* beyond 2^48 bytes: square on from the last cached power */
+                        uint64_t sq[64], u[64];
+                        int c;
+                        memcpy(sq, p2[ZP2_BITS - 1], sizeof(sq));
+                        for (c = ZP2_BITS - 1; c < b; c++) {
+                                compose(sq, sq, u);
+                                memcpy(sq, u, sizeof(u));
+                        }
                         compose(sq, acc, t);
-                        memcpy(acc, t, sizeof(t));
                 }
-                n >>= 1;
-                if (n) {
-                        compose(sq, sq, t);
-                        memcpy(sq, t, sizeof(t));
-                }
+                memcpy(acc, t, sizeof(t));
         }
         memcpy(out, acc, sizeof(acc));
+}
+
+/* Z^n applied to one register value: one map per set bit of n. */
+static uint64_t
+zapply(int variant, unsigned long long n, uint64_t v)
+{
+        const uint64_t (*p2)[64] = zpow2(variant);
+        int b;
+        for (b = 0; n && b < ZP2_BITS; b++, n >>= 1)
+                if (n & 1)
+                        v = apply(p2[b], v);
+        if (n) { /* beyond 2^48 bytes */
+                uint64_t m[64];
+                isal_hip_crc64_zpow(variant, n << ZP2_BITS, m);
+                v = apply(m, v);
+        }
+        return v;
 }
 
 static int
@@ -194,6 +243,22 @@ slice_tables(int variant, uint64_t *tabs)
                 }
 }
 
+/* The maps that depend on the length and the geometry: OP_BLOCK, OP_LAST and
+ * OP_TAIL (the rest of the table set depends on the flavour only). */
+void
+isal_hip_crc64_len_tables(int variant, long long len, int tt, uint64_t *tabs)
+{
+        uint64_t m[64];
+        isal_hip_crc64_geom g;
+        isal_hip_crc64_geometry(len, tt, &g);
+        isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * g.tt, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_OP_BLOCK);
+        isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * g.nfull_last, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_OP_LAST);
+        isal_hip_crc64_zpow(variant, (unsigned long long) (g.tail / 16) * 16, m);
+        op_tables(m, tabs + ISAL_HIP_CRC64_OP_TAIL);
+}
+
 /* Layout: isal_hip_internal.h (ISAL_HIP_CRC64_*). */
 void
 isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
@@ -232,16 +297,11 @@ isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
         isal_hip_crc64_zpow(variant, 4ULL * ISAL_HIP_CRC_TILE, m);
         op_tables(m, tabs + ISAL_HIP_CRC64_SHIFTX_TAB + ISAL_HIP_CRC64_OP_ENTRIES);
         /* combine plan */
-        isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * g.tt, m);
-        op_tables(m, tabs + ISAL_HIP_CRC64_OP_BLOCK);
-        isal_hip_crc64_zpow(variant, (unsigned long long) ISAL_HIP_CRC_TILE * g.nfull_last, m);
-        op_tables(m, tabs + ISAL_HIP_CRC64_OP_LAST);
+        isal_hip_crc64_len_tables(variant, len, tt, tabs);
         for (s = 0; s < 8; s++) {
                 isal_hip_crc64_zpow(variant, 16ULL << s, m);
                 op_tables(m, tabs + ISAL_HIP_CRC64_OP_TREE + s * ISAL_HIP_CRC64_OP_ENTRIES);
         }
-        isal_hip_crc64_zpow(variant, (unsigned long long) (g.tail / 16) * 16, m);
-        op_tables(m, tabs + ISAL_HIP_CRC64_OP_TAIL);
         slice_tables(variant, tabs);
         /* pre-shifted field tables (u-domain) of the checksum-only kernel */
         isal_hip_crc64_zpow(variant, ISAL_HIP_CRC_TILE - 16, m);
@@ -254,6 +314,25 @@ isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs)
                 chunk_tables(bu, tabs + ISAL_HIP_CRC64_PRE_TAB);
                 chunk_tables(bz, tabs + ISAL_HIP_CRC64_PRE_TAB + ISAL_HIP_CRC64_CHUNK_ENTRIES);
         }
+}
+
+/* Tables of the CPU route (crc_cpu.c): the reference's byte table and the
+ * slicing-by-8 tables A_j[v] = pi(raw(0, v at byte j of 8)) (the u-domain step
+ * of slice_tables above, without the pre-shifted half). */
+void
+isal_hip_crc64_cpu_tables(int variant, uint64_t byte[256], uint64_t slice[8 * 256])
+{
+        uint8_t d[8];
+        int j, v;
+        for (v = 0; v < 256; v++)
+                byte[v] = raw_update(variant, isal_hip_crc64_is_refl(variant) ? (uint64_t) v : (uint64_t) v << 56,
+                                     NULL, 1);
+        for (j = 0; j < 8; j++)
+                for (v = 0; v < 256; v++) {
+                        memset(d, 0, sizeof(d));
+                        d[j] = (uint8_t) v;
+                        slice[j * 256 + v] = pi_of(variant, raw_update(variant, 0, d, 8));
+                }
 }
 
 void
@@ -270,7 +349,5 @@ isal_hip_crc64_geometry(long long len, int tt, isal_hip_crc64_geom *g)
 uint64_t
 isal_hip_crc64_init_term(int variant, long long len, uint64_t init)
 {
-        uint64_t m[64];
-        isal_hip_crc64_zpow(variant, (unsigned long long) len, m);
-        return apply(m, ~init);
+        return zapply(variant, (unsigned long long) len, ~init);
 }

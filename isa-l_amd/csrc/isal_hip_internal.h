@@ -316,9 +316,18 @@ typedef struct {
 } isal_hip_crc64_geom;
 
 int isal_hip_crc64_is_refl(int variant);
+void isal_hip_crc64_cpu_tables(int variant, uint64_t byte[256], uint64_t slice[8 * 256]);
+
+/* ---- the checksum entry points' CPU route (crc_cpu.c): host buffers --------
+ * crc32_iscsi semantics (register starts at init, no inversion) and
+ * crc64_<variant> semantics (starts at ~init, inverted on return). */
+uint32_t isal_cpu_crc32c(uint32_t init, const unsigned char *buf, uint64_t len);
+uint64_t isal_cpu_crc64(int variant, uint64_t init, const unsigned char *buf, uint64_t len);
 void isal_hip_crc64_geometry(long long len, int tt, isal_hip_crc64_geom *g);
 void isal_hip_crc64_zpow(int variant, unsigned long long n, uint64_t out[64]);
 void isal_hip_crc64_tables(int variant, long long len, int tt, uint64_t *tabs);
+/* only OP_BLOCK, OP_LAST and OP_TAIL (the length / geometry dependent maps) */
+void isal_hip_crc64_len_tables(int variant, long long len, int tt, uint64_t *tabs);
 uint64_t isal_hip_crc64_init_term(int variant, long long len, uint64_t init);
 
 /* crc64(init, shard, len) of the nsh shards of each stripe (d_ptrs row

@@ -40,6 +40,8 @@
 #include <string.h>
 #include <time.h>
 
+#include "crc.h"
+#include "crc64.h"
 #include "erasure_code.h"
 #include "isal_hip.h"
 #include "isal_hip_internal.h"
@@ -281,6 +283,15 @@ typedef struct {
         void *h_mail_dev;
         unsigned long long seq;
         int unsynced;
+        /* checksum entry points on device buffers: kernel tables of the last
+         * geometry per flavour (CRC32C, the eight CRC64) and the partials */
+        struct crcc {
+                long long len;
+                int tt;
+                void *d_tabs;
+        } c32, c64[ISAL_HIP_CRC64_NVARIANTS];
+        void *d_cpart;
+        size_t cpart_cap;
 } ctx_t;
 
 /* Copy-out worker of a calling thread. The runtime serves a copy from or to
@@ -370,6 +381,13 @@ ctx_free(ctx_t *c)
                 (void) hipHostFree((void *) c->h_mail);
         if (c->oq)
                 outq_stop(c);
+        if (c->c32.d_tabs)
+                (void) hipFree(c->c32.d_tabs);
+        for (int v = 0; v < ISAL_HIP_CRC64_NVARIANTS; v++)
+                if (c->c64[v].d_tabs)
+                        (void) hipFree(c->c64[v].d_tabs);
+        if (c->d_cpart)
+                (void) hipFree(c->d_cpart);
         free(c->jobs);
         free(c->tcoef);
         free(c->ttbl);
@@ -1584,6 +1602,14 @@ now_s(void)
  * a slow one is simply waited for. The stream is still synchronised every
  * SYNC_EVERY calls (the kernels have long ended by then) so the runtime
  * retires its launch records. */
+static unsigned long long g_slow_waits;
+
+unsigned long long
+isal_hip_slow_waits(void)
+{
+        return __atomic_load_n(&g_slow_waits, __ATOMIC_RELAXED);
+}
+
 #define DONE_SPIN_S 0.02
 #define DONE_YIELD_S 50e-6 /* then yield the CPU between polls: callers may outnumber cores */
 #define DONE_SYNC_EVERY 64
@@ -1610,6 +1636,7 @@ wait_done(ctx_t *c, unsigned long long seq)
                 }
         }
         if (c->h_mail[0] != seq) {
+                __atomic_add_fetch(&g_slow_waits, 1ull, __ATOMIC_RELAXED);
                 if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
                         return e;
                 c->unsynced = 0;
@@ -2449,6 +2476,332 @@ batch_encode_crc_impl(isal_hip_batch *b, unsigned int init, unsigned int *crc, v
         }
         return batch_crc_finish(b, init, crc, stream);
 }
+
+/* ---- checksum entry points (crc.h, crc64.h) --------------------------------
+ * The reference's crc32_iscsi (include/crc.h:136-150) and crc64_* flavours
+ * (include/crc64.h:54-163, isa-l.def:75-122), routed like ec_encode_data: a
+ * buffer in device memory (hipMalloc or managed) is checksummed by the GPU
+ * kernels of the batch API (crc_kernels.hip, crc64_kernels.hip) on the device
+ * that holds it — one shard, pointer table and result in the thread's pinned
+ * argument buffer, one stream synchronisation — and a host buffer by the CPU
+ * route (crc_cpu.c), where the PCIe copy would cost more than the arithmetic.
+ * The kernel tables of each flavour are kept per thread and device for the
+ * last length (they depend on it); a storage caller checksums fragment after
+ * fragment of one length. A failing HIP call on a device buffer aborts (no
+ * CPU route can read it), as for the erasure-code calls. */
+
+static int crc_tiles(int len, int nstripes, int def);
+
+static hipError_t
+ensure_cpart(ctx_t *c, size_t bytes)
+{
+        hipError_t e;
+        if (bytes <= c->cpart_cap)
+                return hipSuccess;
+        if (c->d_cpart)
+                (void) hipFree(c->d_cpart);
+        c->d_cpart = NULL;
+        c->cpart_cap = 0;
+        if ((e = hipMalloc(&c->d_cpart, bytes)) != hipSuccess)
+                return e;
+        c->cpart_cap = bytes;
+        return hipSuccess;
+}
+
+/* The device a checksum buffer lives on (-1: host memory, the CPU route). */
+static int
+crc_device(const void *buf, uint64_t len)
+{
+        int kind, dev, cur;
+        uintptr_t rb;
+        size_t rs;
+        if (!buf || !len || !gpu_present())
+                return -1;
+        (void) classify(buf, (size_t) len, &kind, &dev, &rb, &rs);
+        if (kind == CL_DEVICE)
+                return dev;
+        if (kind == CL_MANAGED && hipGetDevice(&cur) == hipSuccess)
+                return cur;
+        (void) hipGetLastError();
+        return -1;
+}
+
+#define CRC_GPU_TRY(fn, what, call)                                                                \
+        do {                                                                                       \
+                hipError_t e_ = (call);                                                            \
+                if (e_ != hipSuccess) {                                                            \
+                        fprintf(stderr, "isal_hip: %s: ", fn);                                     \
+                        die(what, e_);                                                             \
+                }                                                                                  \
+        } while (0)
+
+/* crc64_<variant>(init, buf, len) of a buffer on device dev, len <= INT_MAX. */
+static uint64_t
+gpu_crc64_piece(const char *fn, int dev, int variant, uint64_t init, const unsigned char *buf, int len)
+{
+        const int tt = crc_tiles(len, 1, 64);
+        isal_hip_crc64_geom g;
+        struct crcc *cc;
+        hipError_t err = hipSuccess;
+        const char *what = NULL;
+        ctx_t *c;
+        uint64_t *h;
+        c = ctx_get(dev, &err, &what);
+        if (!c) {
+                fprintf(stderr, "isal_hip: %s: ", fn);
+                die(what, err);
+        }
+        cc = &c->c64[variant];
+        isal_hip_crc64_geometry(len, tt, &g);
+        if (!cc->d_tabs || cc->len != len || cc->tt != tt) {
+                /* the flavour's tables once, then per length only the maps that
+                 * depend on it (OP_BLOCK, OP_LAST, OP_TAIL: ~0.3 ms, not ~4) */
+                const size_t tb = (size_t) ISAL_HIP_CRC64_TAB_ENTRIES * 8,
+                             op = (size_t) ISAL_HIP_CRC64_OP_ENTRIES * 8;
+                const int full = !cc->d_tabs || cc->len < 0;
+                uint64_t *t = (uint64_t *) malloc(tb);
+                if (!t) {
+                        fprintf(stderr, "isal_hip: out of host memory\n");
+                        abort();
+                }
+                if (full)
+                        isal_hip_crc64_tables(variant, len, tt, t);
+                else
+                        isal_hip_crc64_len_tables(variant, len, tt, t);
+                cc->len = -1;
+                if (!cc->d_tabs)
+                        CRC_GPU_TRY(fn, "hipMalloc (checksum tables)", hipMalloc(&cc->d_tabs, tb));
+                /* the thread's earlier checksum calls have completed (each one
+                 * synchronises), so the tables may be overwritten */
+                if (full) {
+                        CRC_GPU_TRY(fn, "hipMemcpy (checksum tables)",
+                                    hipMemcpy(cc->d_tabs, t, tb, hipMemcpyHostToDevice));
+                } else {
+                        CRC_GPU_TRY(fn, "hipMemcpy (checksum tables)",
+                                    hipMemcpy((uint64_t *) cc->d_tabs + ISAL_HIP_CRC64_OP_BLOCK,
+                                              t + ISAL_HIP_CRC64_OP_BLOCK, 2 * op, hipMemcpyHostToDevice));
+                        CRC_GPU_TRY(fn, "hipMemcpy (checksum tables)",
+                                    hipMemcpy((uint64_t *) cc->d_tabs + ISAL_HIP_CRC64_OP_TAIL,
+                                              t + ISAL_HIP_CRC64_OP_TAIL, op, hipMemcpyHostToDevice));
+                }
+                free(t);
+                cc->len = len;
+                cc->tt = tt;
+        }
+        CRC_GPU_TRY(fn, "hipMalloc (checksum partials)", ensure_cpart(c, (size_t) (g.nblk ? g.nblk : 1) * 256 * 8));
+        CRC_GPU_TRY(fn, "argument buffer", ensure_args(c, 64));
+        h = (uint64_t *) c->h_args;
+        h[0] = (uint64_t) (uintptr_t) buf;
+        h[2] = 0;
+        CRC_GPU_TRY(fn, "crc64 launch",
+                    (hipError_t) isal_hip_launch_crc64((const uint64_t *) c->h_args_dev, 1, 1, 1, len,
+                                                       ((uintptr_t) buf & 15) == 0, isal_hip_crc64_is_refl(variant),
+                                                       tt, (const uint64_t *) cc->d_tabs, (uint64_t *) c->d_cpart,
+                                                       isal_hip_crc64_init_term(variant, len, init),
+                                                       (uint64_t *) c->h_args_dev + 2,
+                                                       c->stream));
+        CRC_GPU_TRY(fn, "hipStreamSynchronize (checksum)", hipStreamSynchronize(c->stream));
+        return h[2];
+}
+
+/* ISAL_HIP_BACKEND=gpu: a host buffer is copied into the thread's staging
+ * buffer on its current device, piece by piece, and checksummed there (the
+ * kernels for every call, as for the erasure-code calls; tests). Returns the
+ * staging address of [buf, buf + n) and the device in *dev. */
+static const unsigned char *
+crc_stage(const char *fn, const unsigned char *buf, size_t n, int *dev)
+{
+        hipError_t err = hipSuccess;
+        const char *what = NULL;
+        ctx_t *c;
+        if (hipGetDevice(dev) != hipSuccess || !(c = ctx_get(*dev, &err, &what))) {
+                fprintf(stderr, "isal_hip: %s: ", fn);
+                die(what ? what : "hipGetDevice", err != hipSuccess ? err : hipErrorNoDevice);
+        }
+        CRC_GPU_TRY(fn, "hipMalloc (staging)", ensure_stage(c, n));
+        CRC_GPU_TRY(fn, "hipMemcpyAsync (staging)", hipMemcpyAsync(c->d_stage, buf, n, hipMemcpyHostToDevice, c->stream));
+        return c->d_stage;
+}
+
+static int
+crc_staged(const unsigned char *buf, uint64_t len)
+{
+        return len && buf && backend() == BACKEND_GPU && gpu_present();
+}
+
+static uint64_t
+crc64_route(const char *fn, int variant, uint64_t init, const unsigned char *buf, uint64_t len)
+{
+        const int dev = crc_device(buf, len);
+        int prev;
+        if (dev < 0 && crc_staged(buf, len)) {
+                const uint64_t piece = stage_limit();
+                int sdev;
+                while (len) {
+                        const uint64_t n = len < piece ? len : piece;
+                        const unsigned char *d = crc_stage(fn, buf, (size_t) n, &sdev);
+                        uint64_t left = n;
+                        while (left) { /* the kernels take an int length */
+                                const int m = left > ((uint64_t) 1 << 30) ? 1 << 30 : (int) left;
+                                init = gpu_crc64_piece(fn, sdev, variant, init, d, m);
+                                d += m;
+                                left -= (uint64_t) m;
+                        }
+                        buf += n;
+                        len -= n;
+                }
+                return init;
+        }
+        if (dev < 0)
+                return isal_cpu_crc64(variant, init, buf, len);
+        if ((prev = isal_hip_dev_enter(dev)) == -2) {
+                fprintf(stderr, "isal_hip: %s: ", fn);
+                die("hipSetDevice (to the device holding the buffer)", hipErrorInvalidDevice);
+        }
+        /* the kernels take an int length: pieces of 1 GiB, chained through the
+         * register (crc64(crc64(init, A), B) = crc64(init, A || B)) */
+        while (len) {
+                const int n = len > ((uint64_t) 1 << 30) ? 1 << 30 : (int) len;
+                init = gpu_crc64_piece(fn, dev, variant, init, buf, n);
+                buf += n;
+                len -= (uint64_t) n;
+        }
+        isal_hip_dev_leave(prev);
+        return init;
+}
+
+static uint32_t
+gpu_crc32c(const char *fn, int dev, uint32_t init, const unsigned char *buf, int len)
+{
+        const int tt = crc_tiles(len, 1, 64);
+        isal_hip_crc_geom g;
+        struct crcc *cc;
+        hipError_t err = hipSuccess;
+        const char *what = NULL;
+        const size_t tab = ISAL_HIP_CRC_TAB_DWORDS,
+                     plan = ISAL_HIP_CRC_PLAN_DWORDS + ISAL_HIP_CRC_EXT_DWORDS + ISAL_HIP_CRC_B16_DWORDS +
+                            ISAL_HIP_CRC_FPRE_DWORDS;
+        size_t part;
+        ctx_t *c;
+        uint32_t *h;
+        c = ctx_get(dev, &err, &what);
+        if (!c) {
+                fprintf(stderr, "isal_hip: %s: ", fn);
+                die(what, err);
+        }
+        cc = &c->c32;
+        isal_hip_crc_geometry(len, tt, &g);
+        if (!cc->d_tabs || cc->len != len || cc->tt != tt) {
+                /* all tables once, then per length only the combine plan */
+                const int full = !cc->d_tabs || cc->len < 0;
+                uint32_t *t = (uint32_t *) malloc((tab + plan) * 4);
+                if (!t) {
+                        fprintf(stderr, "isal_hip: out of host memory\n");
+                        abort();
+                }
+                isal_hip_crc32c_plan(len, tt, t + tab);
+                if (full) {
+                        isal_hip_crc32c_tables(t);
+                        isal_hip_crc32c_ext_tables(t, t + ISAL_HIP_CRC_EXT_TAB);
+                        isal_hip_crc32c_byte_tables(t + ISAL_HIP_CRC_B16_TAB);
+                        isal_hip_crc32c_pre_tables(t, t + ISAL_HIP_CRC_FPRE_TAB);
+                }
+                cc->len = -1;
+                if (!cc->d_tabs)
+                        CRC_GPU_TRY(fn, "hipMalloc (checksum tables)", hipMalloc(&cc->d_tabs, (tab + plan) * 4));
+                if (full)
+                        CRC_GPU_TRY(fn, "hipMemcpy (checksum tables)",
+                                    hipMemcpy(cc->d_tabs, t, (tab + plan) * 4, hipMemcpyHostToDevice));
+                else
+                        CRC_GPU_TRY(fn, "hipMemcpy (checksum tables)",
+                                    hipMemcpy((uint32_t *) cc->d_tabs + tab, t + tab, ISAL_HIP_CRC_PLAN_DWORDS * 4,
+                                              hipMemcpyHostToDevice));
+                free(t);
+                cc->len = len;
+                cc->tt = tt;
+        }
+        part = (size_t) g.nblk * 256;
+        CRC_GPU_TRY(fn, "hipMalloc (checksum partials)", ensure_cpart(c, (part + 256) * 4));
+        CRC_GPU_TRY(fn, "argument buffer", ensure_args(c, 64));
+        ((uint64_t *) c->h_args)[0] = (uint64_t) (uintptr_t) buf;
+        h = (uint32_t *) c->h_args + 4;
+        *h = 0;
+        CRC_GPU_TRY(fn, "crc32c launch",
+                    (hipError_t) isal_hip_launch_crc((const uint64_t *) c->h_args_dev, 1, 0, 1, 1, len,
+                                                     ((uintptr_t) buf & 15) == 0, tt, (const uint32_t *) cc->d_tabs,
+                                                     (uint32_t *) c->d_cpart, (uint32_t *) c->d_cpart + part, 1, 0,
+                                                     c->stream));
+        CRC_GPU_TRY(fn, "crc32c combine launch",
+                    (hipError_t) isal_hip_launch_crc_combine((const uint32_t *) c->d_cpart,
+                                                             (const uint32_t *) c->d_cpart + part,
+                                                             (const uint32_t *) cc->d_tabs + tab, g.nblk, g.tail != 0,
+                                                             init, (uint32_t *) c->h_args_dev + 4, 1, c->stream));
+        CRC_GPU_TRY(fn, "hipStreamSynchronize (checksum)", hipStreamSynchronize(c->stream));
+        return *h;
+}
+
+static unsigned int
+crc32c_route(const char *fn, const unsigned char *buf, int len, unsigned int init)
+{
+        int dev, prev;
+        unsigned int r;
+        if (len <= 0)
+                return init; /* the reference's loop runs no byte */
+        dev = crc_device(buf, (uint64_t) len);
+        if (dev < 0 && crc_staged(buf, (uint64_t) len)) {
+                const int piece = stage_limit() < ((size_t) 1 << 30) ? (int) stage_limit() : 1 << 30;
+                int sdev;
+                /* crc32_iscsi chains through its register: crc(crc(init, A), B) = crc(init, A || B) */
+                while (len) {
+                        const int n = len < piece ? len : piece;
+                        const unsigned char *d = crc_stage(fn, buf, (size_t) n, &sdev);
+                        init = gpu_crc32c(fn, sdev, init, d, n);
+                        buf += n;
+                        len -= n;
+                }
+                return init;
+        }
+        if (dev < 0)
+                return isal_cpu_crc32c(init, buf, (uint64_t) len);
+        if ((prev = isal_hip_dev_enter(dev)) == -2) {
+                fprintf(stderr, "isal_hip: %s: ", fn);
+                die("hipSetDevice (to the device holding the buffer)", hipErrorInvalidDevice);
+        }
+        r = gpu_crc32c(fn, dev, init, buf, len);
+        isal_hip_dev_leave(prev);
+        return r;
+}
+
+unsigned int
+crc32_iscsi(unsigned char *buffer, int len, unsigned int init_crc)
+{
+        return crc32c_route("crc32_iscsi", buffer, len, init_crc);
+}
+
+unsigned int
+crc32_iscsi_base(unsigned char *buffer, int len, unsigned int crc_init)
+{
+        return crc32c_route("crc32_iscsi_base", buffer, len, crc_init);
+}
+
+#define CRC64_ENTRY(name, variant)                                                                 \
+        uint64_t name(uint64_t init_crc, const unsigned char *buf, uint64_t len)                   \
+        {                                                                                          \
+                return crc64_route(#name, variant, init_crc, buf, len);                            \
+        }                                                                                          \
+        uint64_t name##_base(uint64_t init_crc, const unsigned char *buf, uint64_t len)            \
+        {                                                                                          \
+                return crc64_route(#name "_base", variant, init_crc, buf, len);                    \
+        }
+CRC64_ENTRY(crc64_ecma_refl, ISAL_HIP_CRC64_ECMA_REFL)
+CRC64_ENTRY(crc64_ecma_norm, ISAL_HIP_CRC64_ECMA_NORM)
+CRC64_ENTRY(crc64_iso_refl, ISAL_HIP_CRC64_ISO_REFL)
+CRC64_ENTRY(crc64_iso_norm, ISAL_HIP_CRC64_ISO_NORM)
+CRC64_ENTRY(crc64_jones_refl, ISAL_HIP_CRC64_JONES_REFL)
+CRC64_ENTRY(crc64_jones_norm, ISAL_HIP_CRC64_JONES_NORM)
+CRC64_ENTRY(crc64_rocksoft_refl, ISAL_HIP_CRC64_ROCKSOFT_REFL)
+CRC64_ENTRY(crc64_rocksoft_norm, ISAL_HIP_CRC64_ROCKSOFT_NORM)
+#undef CRC64_ENTRY
 
 /* ---- the batch entry points run on the batch's device -------------------- */
 

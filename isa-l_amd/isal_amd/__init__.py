@@ -28,7 +28,7 @@ __all__ = [
     "gf_vect_dot_prod", "gf_vect_dot_prod_base", "gf_vect_mad", "gf_vect_mad_base",
     "gf_vect_mul", "gf_vect_mul_base", "Batch", "Pipe", "kernel_launches", "max_rows_per_pass",
     "version", "addr", "cpu_calls", "fallbacks", "reload_config", "Multi", "partition",
-    "route_device", "contexts_created", "selftest_kernels",
+    "route_device", "contexts_created", "selftest_kernels", "crc32_iscsi", "crc64", "CRC64_VARIANTS", "slow_waits",
 ]
 
 LIB_PATH = os.environ.get(
@@ -128,8 +128,14 @@ def lib() -> ctypes.CDLL:
             "isal_hip_route_device": (i, [i, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), i,
                                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
             "isal_hip_contexts_created": (ctypes.c_ulonglong, []),
+            "isal_hip_slow_waits": (ctypes.c_ulonglong, []),
             "isal_hip_selftest_kernels": (i, [ctypes.POINTER(ctypes.c_int)]),
+            "crc32_iscsi": (ctypes.c_uint, [ctypes.c_void_p, i, ctypes.c_uint]),
+            "crc32_iscsi_base": (ctypes.c_uint, [ctypes.c_void_p, i, ctypes.c_uint]),
         }
+        for v in CRC64_VARIANTS:
+            for suffix in ("", "_base"):
+                sig[f"crc64_{v}{suffix}"] = (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64])
         for name, (res, args) in sig.items():
             f = getattr(L, name)
             f.restype = res
@@ -465,6 +471,21 @@ def numa_node_cpus(node: int, sysfs_root: str | None = None) -> list[int] | None
     return None if n < 0 else list(buf[:min(n, 4096)])
 
 
+def crc32_iscsi(buf, len_: int, init_crc: int, base: bool = False) -> int:
+    """crc.h crc32_iscsi(buffer, len, init_crc) (reference include/crc.h:136-150):
+    host buffers on the library's CPU route, device buffers on the GPU."""
+    f = lib().crc32_iscsi_base if base else lib().crc32_iscsi
+    return int(f(ctypes.c_void_p(addr(buf) if buf is not None else 0), len_, init_crc & 0xFFFFFFFF))
+
+
+def crc64(variant, init_crc: int, buf, len_: int, base: bool = False) -> int:
+    """crc64.h crc64_<variant>(init_crc, buf, len) (reference include/crc64.h:54-163);
+    variant: a CRC64_VARIANTS name or its index (ISAL_HIP_CRC64_*)."""
+    name = variant if isinstance(variant, str) else CRC64_VARIANTS[variant]
+    f = getattr(lib(), f"crc64_{name}{'_base' if base else ''}")
+    return int(f(init_crc & 0xFFFFFFFFFFFFFFFF, ctypes.c_void_p(addr(buf) if buf is not None else 0), len_))
+
+
 MEM_PAGEABLE, MEM_DEVICE, MEM_MANAGED, MEM_PINNED = 0, 1, 2, 3
 
 
@@ -486,6 +507,11 @@ def selftest_kernels() -> tuple[int, int]:
     n = ctypes.c_int(0)
     bad = lib().isal_hip_selftest_kernels(ctypes.byref(n))
     return int(bad), int(n.value)
+
+
+def slow_waits() -> int:
+    """Kernel-argument calls completed by hipStreamSynchronize after the spin expired."""
+    return int(lib().isal_hip_slow_waits())
 
 
 def contexts_created() -> int:

@@ -9,7 +9,7 @@ import pytest
 
 import ecutil
 
-HEADERS = ["erasure_code.h", "gf_vect_mul.h", "isal_api.h", "isal_hip.h", "raid.h"]
+HEADERS = ["erasure_code.h", "gf_vect_mul.h", "isal_api.h", "isal_hip.h", "raid.h", "crc.h", "crc64.h"]
 
 # Reference data-path + support symbols the boundary must provide (SURVEY.md §8b,
 # reference isa-l.def:5-57,114-124 restricted to erasure coding).

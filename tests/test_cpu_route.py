@@ -221,7 +221,7 @@ def test_pq_check_every_corruption_position(cpu_engine, oracle):
 CONFORMANCE = ["gf_inverse_test", "gf_vect_mul_test", "gf_vect_mul_base_test",
                "gf_vect_dot_prod_base_test", "gf_vect_dot_prod_test", "gf_vect_mad_test",
                "erasure_code_base_test", "erasure_code_test", "erasure_code_update_test",
-               "xor_gen_test", "pq_gen_test", "xor_check_test", "pq_check_test"]
+               "xor_gen_test", "pq_gen_test", "xor_check_test", "pq_check_test", "crc64_funcs_test"]
 
 
 def run_programs(directory, names, env, timeout=600):
@@ -268,3 +268,63 @@ def test_bench_c1_cpu_plumbing():
     assert out["parity_matches_fixture"] is True and out["value"] > 0
     if out["cpu_baseline"] is not None:
         assert out["cpu_baseline"]["parity_matches_fixture"] is True
+
+
+# --------------------------------------------------------------------------
+# checksum entry points (crc.h / crc64.h) on host buffers: the CPU route
+# --------------------------------------------------------------------------
+
+def _crc_lengths():
+    return list(range(0, 301)) + [511, 4095, 4096, 4097, 65536 + 7, 1 << 20]
+
+
+@pytest.mark.parametrize("simd", ["1", "0"])
+def test_crc32_iscsi_host_route_vs_oracle(engine, oracle, monkeypatch, simd):
+    """crc32_iscsi / _base (reference include/crc.h:136-150) on host buffers:
+    == the oracle's restatement of crc_base.c:205-219 at lengths 0..300 and
+    beyond, misaligned starts, random inits; the SSE4.2 path and (CPU_SIMD=0)
+    the slicing-by-8 tables; the committed reference fixtures."""
+    monkeypatch.setenv("ISAL_HIP_CPU_SIMD", simd)
+    engine.reload_config()
+    rng = np.random.default_rng(5)
+    big = fill_bytes((1 << 20) + 64, 77)
+    for n in _crc_lengths():
+        off = int(rng.integers(0, 16))
+        a = np.ascontiguousarray(big[off: off + n])
+        init = int(rng.integers(0, 1 << 32))
+        want = oracle.crc32_iscsi(a, init)
+        assert engine.crc32_iscsi(a, n, init) == want, (n, off)
+        assert engine.crc32_iscsi(a, n, init, base=True) == want, (n, off)
+    assert engine.crc32_iscsi(None, 0, 0x1234) == 0x1234
+    assert engine.crc32_iscsi(big, -5, 0x1234) == 0x1234  # no byte runs for len <= 0
+    for case in golden().get("crc32_iscsi", []):
+        a = ecutil.crc_fixture_bytes(case)
+        assert engine.crc32_iscsi(a, a.size, case["init"]) == case["crc"], case.get("len")
+    monkeypatch.undo()
+    engine.reload_config()
+
+
+@pytest.mark.parametrize("variant", range(8))
+def test_crc64_host_route_vs_oracle(engine, oracle, variant):
+    """crc64_<flavour> / _base (reference include/crc64.h:54-163) on host
+    buffers: == the oracle's restatement of crc64_base.c at lengths 0..300
+    and beyond, misaligned starts, random inits; chaining
+    crc(crc(init, A), B) == crc(init, A || B); the reference fixtures."""
+    rng = np.random.default_rng(100 + variant)
+    big = fill_bytes((1 << 20) + 64, 88)
+    for n in _crc_lengths():
+        off = int(rng.integers(0, 16))
+        a = np.ascontiguousarray(big[off: off + n])
+        init = int(rng.integers(0, 1 << 63)) * 2 + int(rng.integers(0, 2))
+        want = oracle.crc64(variant, a, init)
+        assert engine.crc64(variant, init, a, n) == want, (variant, n, off)
+        assert engine.crc64(variant, init, a, n, base=True) == want, (variant, n, off)
+    a = big[:100000]
+    cut = 31337
+    assert engine.crc64(variant, engine.crc64(variant, 7, a[:cut], cut), np.ascontiguousarray(a[cut:]),
+                        a.size - cut) == engine.crc64(variant, 7, a, a.size)
+    assert engine.crc64(variant, 0, None, 0) == 0
+    for case in golden().get("crc64", []):
+        if case["variant"] == variant:
+            b = ecutil.crc_fixture_bytes(case)
+            assert engine.crc64(variant, int(case["init"]), b, b.size) == int(case["crc"]), case.get("len")

@@ -1440,7 +1440,7 @@ def test_config_c4_pipeline_full_shape_vs_oracle(engine, oracle, gpu):
 CONFORMANCE = ["gf_inverse_test", "gf_vect_mul_test", "gf_vect_mul_base_test",
                "gf_vect_dot_prod_base_test", "gf_vect_dot_prod_test", "gf_vect_mad_test",
                "erasure_code_base_test", "erasure_code_test", "erasure_code_update_test",
-               "xor_gen_test", "pq_gen_test", "xor_check_test", "pq_check_test"]
+               "xor_gen_test", "pq_gen_test", "xor_check_test", "pq_check_test", "crc64_funcs_test"]
 
 
 # xor_check_test / pq_check_test sweep every (length, error position, vector)
@@ -2251,3 +2251,120 @@ def test_selftest_every_launchable_kernel_resolves(engine, gpu):
     bad, n = engine.selftest_kernels()
     assert n > 800, n
     assert bad == 0, f"{bad} of {n} kernels have no usable device code (named on stderr)"
+
+
+# --------------------------------------------------------------------------
+# checksum entry points (crc.h / crc64.h) on device buffers
+# --------------------------------------------------------------------------
+
+_CRC_DEV_LENGTHS = list(range(0, 301)) + [4095, 4096, 4097, 65536 + 7, 1 << 20, (1 << 20) + 3]
+
+
+def test_crc_entry_points_device_buffers_vs_oracle(engine, oracle, gpu):
+    """crc32_iscsi / crc64_* and their _base twins (reference include/crc.h:
+    136-150, include/crc64.h:54-163) on DEVICE buffers run the GPU checksum
+    kernels: == the oracle at lengths 0..300, around a tile and at 1 MiB, from
+    misaligned starts, with random inits, all eight CRC64 flavours."""
+    import torch
+
+    rng = np.random.default_rng(2024)
+    host = fill_bytes((1 << 20) + 64, 4242)
+    dev = torch.from_numpy(host).to(gpu)
+    launches = engine.kernel_launches()
+    for n in _CRC_DEV_LENGTHS:
+        off = int(rng.integers(0, 16))
+        a = host[off: off + n]
+        p = dev.data_ptr() + off
+        i32 = int(rng.integers(0, 1 << 32))
+        want = oracle.crc32_iscsi(a, i32)
+        assert engine.crc32_iscsi(p, n, i32) == want, ("crc32_iscsi", n, off)
+        assert engine.crc32_iscsi(p, n, i32, base=True) == want, ("crc32_iscsi_base", n, off)
+        for v in range(8):
+            i64 = int(rng.integers(0, 1 << 62)) * 4 + v
+            want = oracle.crc64(v, a, i64)
+            assert engine.crc64(v, i64, p, n) == want, (engine.CRC64_VARIANTS[v], n, off)
+            if n % 7 == 0:
+                assert engine.crc64(v, i64, p, n, base=True) == want, (v, n, off)
+    assert engine.kernel_launches() > launches, "the GPU checksum kernels did not run"
+
+
+def test_crc_entry_points_host_buffers_staged_under_gpu_backend(engine, oracle, gpu):
+    """Under ISAL_HIP_BACKEND=gpu (this module's setting) host buffers are staged
+    into HBM and checksummed by the kernels too: == the oracle."""
+    rng = np.random.default_rng(7)
+    launches = engine.kernel_launches()
+    for n in (1, 15, 16, 17, 4096 + 5, 300000):
+        a = fill_bytes(n, n)
+        assert engine.crc32_iscsi(a, n, 0x5A5A5A5A) == oracle.crc32_iscsi(a, 0x5A5A5A5A), n
+        for v in range(8):
+            init = int(rng.integers(0, 1 << 63))
+            assert engine.crc64(v, init, a, n) == oracle.crc64(v, a, init), (v, n)
+    assert engine.kernel_launches() > launches
+
+
+def test_crc64_device_buffer_beyond_one_gib(engine, oracle, gpu):
+    """A device buffer longer than the kernels' int length is checksummed in
+    1 GiB pieces chained through the register: == the oracle."""
+    import torch
+
+    n = (1 << 30) + 4096 * 3 + 5
+    t = torch.empty(n, dtype=torch.uint8, device=gpu)
+    t.random_(generator=torch.Generator(device=gpu).manual_seed(11))
+    h = t.cpu().numpy()
+    assert engine.crc64(0, 0x1234, t.data_ptr(), n) == oracle.crc64(0, h, 0x1234)
+    assert engine.crc32_iscsi(t.data_ptr(), (1 << 30) + 17, 9) == oracle.crc32_iscsi(h[:(1 << 30) + 17], 9)
+
+
+def test_dropin_waits_out_a_slow_stream(engine, oracle, gpu):
+    """The mailbox wait (isal_hip_shim.c wait_done) spins 20 ms, then lets
+    hipStreamSynchronize finish the call. Here > 30 ms of torch work queued on
+    the legacy default stream — ending with the writes of the very source
+    shards — holds the engine's blocking stream back: a drop-in encode and a
+    pq_check on device shards must take that branch (isal_hip_slow_waits) and
+    still return the oracle's results."""
+    import torch
+
+    k, rows, n = 10, 4, 256 << 10
+    coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+    tbls = engine.ec_init_tables(k, rows, coef)
+    want_src = torch.empty((k, n), dtype=torch.uint8, device=gpu)
+    want_src.random_(generator=torch.Generator(device=gpu).manual_seed(31))
+    h = _host(want_src)
+    want = oracle.encode(coef, k, rows, [h[j] for j in range(k)])
+    x = torch.randn((4096, 4096), device=gpu)
+    torch.cuda.synchronize()
+
+    def slow_then(fill):
+        y = x
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(100):  # ~0.14 TFLOP each: ~1 ms apiece
+            y = (y @ x) * 1e-3
+        fill()
+        t1.record()
+        return y, t0, t1
+
+    slow0 = engine.slow_waits()
+    src = torch.zeros((k, n), dtype=torch.uint8, device=gpu)
+    out = torch.zeros((rows, n), dtype=torch.uint8, device=gpu)
+    y, t0, t1 = slow_then(lambda: src.copy_(want_src))
+    engine.ec_encode_data(n, k, rows, tbls, [src[j] for j in range(k)], [out[l] for l in range(rows)])
+    torch.cuda.synchronize()
+    assert t0.elapsed_time(t1) > 30.0, f"queued work too short to outlast the spin: {t0.elapsed_time(t1):.1f} ms"
+    for l in range(rows):
+        assert np.array_equal(_host(out[l]), want[l]), l
+    # pq_check (a verify: its result travels in the mailbox too)
+    v, n2 = 8, 65536
+    bufs = torch.from_numpy(np.stack([fill_bytes(n2, 900 + j) for j in range(v)])).to(gpu)
+    assert _raid_fn(engine, "pq_gen")(v, n2, _vp([bufs[j] for j in range(v)])) == 0
+    ref = [b.cpu().numpy().copy() for b in bufs]
+    ref[3][1234] ^= 0x10
+    bad = torch.from_numpy(np.stack(ref)).to(gpu)
+    chk = torch.zeros_like(bad)
+    torch.cuda.synchronize()
+    y, t0, t1 = slow_then(lambda: chk.copy_(bad))
+    got = _raid_fn(engine, "pq_check")(v, n2, _vp([chk[j] for j in range(v)]))
+    assert got == oracle.raid("pq_check", v, n2, ref), got
+    assert engine.slow_waits() >= slow0 + 2, (slow0, engine.slow_waits())
+    del y
