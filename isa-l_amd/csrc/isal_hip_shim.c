@@ -2048,10 +2048,13 @@ struct isal_hip_batch {
         isal_hip_crc_geom crc;
         uint32_t *d_crc, *d_part, *d_tail;
         /* CRC64 state, allocated on first use: one table set per variant
-         * used (never overwritten, so switching variants needs no device
-         * synchronisation) and the per-lane chains */
-        int c64_tt;
-        uint64_t *d_c64tab[ISAL_HIP_CRC64_NVARIANTS], *d_c64part;
+         * and pass used (never overwritten, so switching variants needs no
+         * device synchronisation) and the per-lane chains. The fused pass
+         * (c64_tt tiles per block) and the checksum-only pass (c64_tt_ck)
+         * have their own block geometry; the partials are sized for the
+         * shorter blocks. */
+        int c64_tt, c64_tt_ck;
+        uint64_t *d_c64tab[ISAL_HIP_CRC64_NVARIANTS], *d_c64tab_ck[ISAL_HIP_CRC64_NVARIANTS], *d_c64part;
 };
 
 /* Every shard of a batch on device dev: hipMalloc memory of dev, managed
@@ -2244,9 +2247,12 @@ isal_hip_batch_destroy(isal_hip_batch *b)
                 (void) hipFree(b->d_crc);
         if (b->d_part)
                 (void) hipFree(b->d_part);
-        for (int v = 0; v < ISAL_HIP_CRC64_NVARIANTS; v++)
+        for (int v = 0; v < ISAL_HIP_CRC64_NVARIANTS; v++) {
                 if (b->d_c64tab[v])
                         (void) hipFree(b->d_c64tab[v]);
+                if (b->d_c64tab_ck[v])
+                        (void) hipFree(b->d_c64tab_ck[v]);
+        }
         if (b->d_c64part)
                 (void) hipFree(b->d_c64part);
         free(b);
@@ -2358,28 +2364,34 @@ batch_crc_impl(isal_hip_batch *b, unsigned int init, unsigned int *crc, void *st
 
 /* ---- CRC64 of the batch's shards (isal_hip.h) ----------------------------- */
 
+/* ck: the checksum-only pass (else the fused encode + CRC64 pass). */
 static int
-batch_crc64_setup(isal_hip_batch *b, int variant)
+batch_crc64_setup(isal_hip_batch *b, int variant, int ck)
 {
         isal_hip_crc64_geom g;
         uint64_t *h, *d = NULL;
         hipError_t e;
         const size_t tab = ISAL_HIP_CRC64_TAB_ENTRIES;
-        if (b->d_c64tab[variant])
+        uint64_t **slot = ck ? &b->d_c64tab_ck[variant] : &b->d_c64tab[variant];
+        if (*slot)
                 return ISAL_HIP_OK;
         if (!b->d_c64part && !b->c64_tt) {
-                /* 64 tiles per block: the checksum-only pass runs 2.7 % faster
-                 * than at 32, the fused pass is flat from 32 to 64
-                 * (profiles/r03/r03_crc_tiles_sweep.jsonl) */
+                /* Tiles per block: the fused pass 64 (flat from 32 to 64,
+                 * profiles/r03/r03_crc_tiles_sweep.jsonl; 128 is 1.2-1.6 %
+                 * slower), the checksum-only pass with its two chains per lane
+                 * 128 (+1.3-1.6 % over 64, profiles/r05/r05_crc64_tiles_ab.txt).
+                 * crc_tiles halves both alike for small batches, so c64_tt_ck
+                 * >= c64_tt and the partials sized for c64_tt hold either. */
                 b->c64_tt = crc_tiles(b->len, b->nstripes, 64);
-                isal_hip_crc64_geometry(b->len, b->c64_tt, &g);
+                b->c64_tt_ck = crc_tiles(b->len, b->nstripes, 128);
+                isal_hip_crc64_geometry(b->len, b->c64_tt < b->c64_tt_ck ? b->c64_tt : b->c64_tt_ck, &g);
                 if (g.nblk) {
                         e = hipMalloc((void **) &b->d_c64part, (size_t) b->nstripes *
                                                                        (size_t) (b->k + b->rows) *
                                                                        (size_t) g.nblk * 256 * 8);
                         if (e != hipSuccess) {
                                 b->d_c64part = NULL;
-                                b->c64_tt = 0; /* retry the whole setup next time */
+                                b->c64_tt = b->c64_tt_ck = 0; /* retry the whole setup next time */
                                 return e == hipErrorOutOfMemory ? ISAL_HIP_ENOMEM : ISAL_HIP_EHIP;
                         }
                 }
@@ -2387,7 +2399,7 @@ batch_crc64_setup(isal_hip_batch *b, int variant)
         h = (uint64_t *) malloc(tab * 8);
         if (!h)
                 return ISAL_HIP_ENOMEM;
-        isal_hip_crc64_tables(variant, b->len, b->c64_tt, h);
+        isal_hip_crc64_tables(variant, b->len, ck ? b->c64_tt_ck : b->c64_tt, h);
         /* a fresh buffer per variant: launches of other variants queued on any
          * stream keep reading their own tables */
         e = hipMalloc((void **) &d, tab * 8);
@@ -2399,7 +2411,7 @@ batch_crc64_setup(isal_hip_batch *b, int variant)
                         (void) hipFree(d);
                 return e == hipErrorOutOfMemory ? ISAL_HIP_ENOMEM : ISAL_HIP_EHIP;
         }
-        b->d_c64tab[variant] = d; /* published only once filled */
+        *slot = d; /* published only once filled */
         return ISAL_HIP_OK;
 }
 
@@ -2410,11 +2422,11 @@ batch_crc64_impl(isal_hip_batch *b, int variant, unsigned long long init,
         int r;
         if (!b || !crc || variant < 0 || variant >= ISAL_HIP_CRC64_NVARIANTS)
                 return ISAL_HIP_EINVAL;
-        if ((r = batch_crc64_setup(b, variant)) != ISAL_HIP_OK)
+        if ((r = batch_crc64_setup(b, variant, 1)) != ISAL_HIP_OK)
                 return r;
         return isal_hip_launch_crc64(b->d_ptrs, b->k + b->rows, b->k + b->rows, b->nstripes,
-                                     b->len, b->vec16, isal_hip_crc64_is_refl(variant), b->c64_tt,
-                                     b->d_c64tab[variant], b->d_c64part,
+                                     b->len, b->vec16, isal_hip_crc64_is_refl(variant), b->c64_tt_ck,
+                                     b->d_c64tab_ck[variant], b->d_c64part,
                                      isal_hip_crc64_init_term(variant, b->len, init),
                                      (uint64_t *) crc, stream)
                        ? ISAL_HIP_EHIP
@@ -2429,7 +2441,7 @@ batch_encode_crc64_impl(isal_hip_batch *b, int variant, unsigned long long init,
         isal_hip_crc64_geom g;
         if (!b || !crc || variant < 0 || variant >= ISAL_HIP_CRC64_NVARIANTS)
                 return ISAL_HIP_EINVAL;
-        if ((r = batch_crc64_setup(b, variant)) != ISAL_HIP_OK)
+        if ((r = batch_crc64_setup(b, variant, 0)) != ISAL_HIP_OK)
                 return r;
         isal_hip_crc64_geometry(b->len, b->c64_tt, &g);
         if (b->vec16 && b->len % 16 == 0 && g.nblk > 0 && b->rows <= EC_MAX_ROWS_PER_PASS &&
