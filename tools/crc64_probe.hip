@@ -33,6 +33,32 @@ FUSED64_STUB(8)
 
 namespace {
 
+__device__ __forceinline__ void bt_offs8(uint32_t w, uint32_t (&o)[4]) {
+  const uint32_t three = 3;
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+      : "=v"(o[0]) : "v"(three), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+      : "=v"(o[1]) : "v"(three), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+      : "=v"(o[2]) : "v"(three), "v"(w));
+  asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+      : "=v"(o[3]) : "v"(three), "v"(w));
+}
+
+__device__ __forceinline__ uint64_t bt_at(const uint64_t* t, int j, uint32_t o) {
+  return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(t) + j * 2048 + o);
+}
+
+__device__ __forceinline__ void bt_slice8(X64& acc, const uint64_t* t, uint32_t lo, uint32_t hi) {
+  uint32_t o[4], q[4];
+  bt_offs8(lo, o);
+  bt_offs8(hi, q);
+  acc.add2(bt_at(t, 0, o[0]), bt_at(t, 1, o[1]));
+  acc.add2(bt_at(t, 2, o[2]), bt_at(t, 3, o[3]));
+  acc.add2(bt_at(t, 4, q[0]), bt_at(t, 5, q[1]));
+  acc.add2(bt_at(t, 6, q[2]), bt_at(t, 7, q[3]));
+}
+
 template <int OA>
 __device__ __forceinline__ uint4 lds_rd16(uint32_t addr) {
   u32x4 x;
@@ -221,6 +247,116 @@ __global__ __launch_bounds__(kBlock) void crc64_pre_roll(const uint64_t* __restr
   }
 }
 
+// Byte tables instead of field tables (the fused kernel's chunk path,
+// crc64_kernels.hip chain_step_sl): 16 byte-indexed lookups per chunk (one
+// SDWA op each) into the u-domain slicing tables A / A' (8 x 256 entries
+// each, 32 KiB), at ~3x bank conflicts — fewer VALU and LDS instructions than
+// the 28 field lookups. NV lane groups of 256 share one table copy.
+template <int PH>
+__device__ __forceinline__ uint64_t bt_step(const uint64_t* lt, uint64_t b, uint32_t w0, uint32_t w1, uint32_t w2,
+                                            uint32_t w3) {
+  X64 u{0u, 0u};
+  X64 c{0u, 0u};
+  bt_slice8(u, lt, w0 ^ static_cast<uint32_t>(b), w1 ^ static_cast<uint32_t>(b >> 32));
+  bt_slice8(c, lt + (PH == 1 ? 0 : 8 * 256), w2 ^ u.lo, w3 ^ u.hi);
+  return c.get();
+}
+
+template <int NI, int B, int NV>
+__global__ __launch_bounds__(kBlock* NV) void crc64_pre_bytes(const uint64_t* __restrict__ ptrs, int ptr_stride,
+                                                              int nsh, int len, unsigned nitems, unsigned nblk,
+                                                              unsigned tt, unsigned nfull, int uswap,
+                                                              const uint64_t* __restrict__ tabs,
+                                                              uint64_t* __restrict__ part) {
+  __shared__ uint64_t lt[16 * 256];  // A, A'
+  load_lds<16 * 256, NV>(lt, tabs + ISAL_HIP_CRC64_SLICE_TAB);
+  __syncthreads();
+  const unsigned tid = threadIdx.x % kBlock;
+  const long long lane = tid * kVec;
+  for (unsigned v = blockIdx.x * NV + threadIdx.x / kBlock; NI * v < nitems; v += gridDim.x * NV) {
+    uint64_t base[NI];
+    unsigned t0[NI], t1[NI], n = ~0u;
+    uint64_t bc[NI];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const unsigned w = NI * v + q;
+      base[q] = 0;
+      t0[q] = t1[q] = 0;
+      if (w < nitems) {
+        const unsigned si = w / nblk, blk = w - si * nblk;
+        const unsigned stripe = si / nsh, i = si - stripe * nsh;
+        base[q] = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
+        t0[q] = blk * tt;
+        t1[q] = t0[q] + tt < nfull ? t0[q] + tt : nfull;
+      }
+      n = min(n, t1[q] - t0[q]);
+      bc[q] = 0;
+    }
+    auto stp = [&](bool last, uint64_t b, const uint4& x) __attribute__((always_inline)) {
+      return last ? bt_step<1>(lt, b, x.x, x.y, x.z, x.w) : bt_step<0>(lt, b, x.x, x.y, x.z, x.w);
+    };
+    unsigned i = 0;
+    for (; i + B <= n; i += B) {
+      uint4 x[NI][B];
+#pragma unroll
+      for (int g = 0; g < B; ++g)
+#pragma unroll
+        for (int q = 0; q < NI; ++q)
+          x[q][g] = load16<kBufNT>(base[q], static_cast<long long>(t0[q] + i + g) * kTile + lane, len);
+#pragma unroll
+      for (int g = 0; g < B; ++g)
+#pragma unroll
+        for (int q = 0; q < NI; ++q) bc[q] = stp(t0[q] + i + g + 1 == t1[q], bc[q], x[q][g]);
+    }
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      for (unsigned j = t0[q] + i; j < t1[q]; ++j)
+        bc[q] = stp(j + 1 == t1[q], bc[q], load16<kBufNT>(base[q], static_cast<long long>(j) * kTile + lane, len));
+      const unsigned w = NI * v + q;
+      if (w < nitems) part[static_cast<size_t>(w) * kBlock + tid] = uswap ? __builtin_bswap64(bc[q]) : bc[q];
+    }
+  }
+}
+
+// Compute only: crc64_pre_roll's arithmetic with the loads replaced by
+// register-made chunks (2 VALU ops per dword): what the LDS lookups and VALU
+// cost with no HBM traffic at all (results not comparable).
+template <int NI>
+__global__ __launch_bounds__(kBlock) void crc64_pre_nomem(const uint64_t* __restrict__ ptrs, int ptr_stride, int nsh,
+                                                          int len, unsigned nitems, unsigned nblk, unsigned tt,
+                                                          unsigned nfull, int uswap, const uint64_t* __restrict__ tabs,
+                                                          uint64_t* __restrict__ part) {
+  __shared__ uint64_t lt[2 * kCE];
+  load_lds<2 * kCE>(lt, tabs + ISAL_HIP_CRC64_PRE_TAB);
+  __syncthreads();
+  auto step = [&](bool last, X64 b, const uint4& x) __attribute__((always_inline)) {
+    X64 c{0u, 0u};
+    if (last)
+      chunk_acc(c, lt, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
+    else
+      chunk_acc(c, lt + kCE, x.x ^ b.lo, x.y ^ b.hi, x.z, x.w);
+    return c;
+  };
+  for (unsigned v = blockIdx.x; NI * v < nitems; v += gridDim.x) {
+    X64 bc[NI];
+    unsigned t1 = tt;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) bc[q] = X64{threadIdx.x * 77u + q, v};
+    for (unsigned i = 0; i < t1; ++i) {
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const uint32_t h = (i * 2654435761u) ^ (threadIdx.x + q);
+        bc[q] = step(i + 1 == t1, bc[q], make_uint4(h, h * 3u, h + 12345u, h ^ 0x5bd1e995u));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const unsigned w = NI * v + q;
+      if (w < nitems) part[static_cast<size_t>(w) * kBlock + threadIdx.x] = bc[q].get();
+    }
+  }
+}
+
 }  // namespace
 
 #define CK(x)                                                                        \
@@ -296,6 +432,18 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((crc64_pre_roll<NI, B>), dim3((nitems + NI - 1) / NI), dim3(kBlock), 0, 0, p, nsh_, nsh_,   \
                        len_, nitems, nblk, tt, nfull, 0, t, part);                                               \
   }
+#define BYTES(NI, B, NV)                                                                                         \
+  [](const uint64_t* p, int nsh_, int len_, int, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull,   \
+     const uint64_t* t, uint64_t* part) {                                                                        \
+    hipLaunchKernelGGL((crc64_pre_bytes<NI, B, NV>), dim3((nitems + NI * NV - 1) / (NI * NV)), dim3(kBlock * NV), 0, \
+                       0, p, nsh_, nsh_, len_, nitems, nblk, tt, nfull, 0, t, part);                              \
+  }
+#define NOMEM(NI)                                                                                                 \
+  [](const uint64_t* p, int nsh_, int len_, int, unsigned nitems, unsigned nblk, unsigned tt, unsigned nfull,   \
+     const uint64_t* t, uint64_t* part) {                                                                        \
+    hipLaunchKernelGGL((crc64_pre_nomem<NI>), dim3((nitems + NI - 1) / NI), dim3(kBlock), 0, 0, p, nsh_, nsh_,     \
+                       len_, nitems, nblk, tt, nfull, 0, t, part);                                               \
+  }
   const V vs[] = {
       {"lib", 64, LIB(64)},         {"lib128", 128, LIB(128)},      {"ring4_2", 64, RING(4, 2)},
       {"ring6_2", 64, RING(6, 2)},  {"ring8_2", 64, RING(8, 2)},    {"ring12_2", 64, RING(12, 2)},
@@ -304,6 +452,10 @@ int main(int argc, char** argv) {
       {"roll2_4", 64, ROLL(2, 4)},  {"roll2_2", 64, ROLL(2, 2)},    {"roll2_3", 64, ROLL(2, 3)},
       {"roll1_4", 64, ROLL(1, 4)},  {"roll2_6", 64, ROLL(2, 6)},    {"roll3_2", 64, ROLL(3, 2)},
       {"roll2_4_128", 128, ROLL(2, 4)}, {"roll2_2_128", 128, ROLL(2, 2)},
+      {"bytes2_4_1", 64, BYTES(2, 4, 1)}, {"bytes2_4_2", 64, BYTES(2, 4, 2)}, {"bytes1_4_2", 64, BYTES(1, 4, 2)},
+      {"bytes2_2_2", 64, BYTES(2, 2, 2)}, {"bytes3_2_2", 64, BYTES(3, 2, 2)}, {"bytes2_4_2_128", 128, BYTES(2, 4, 2)},
+      {"bytes4_2_2", 64, BYTES(4, 2, 2)},
+      {"nomem2", 64, NOMEM(2)}, {"nomem1", 64, NOMEM(1)}, {"nomem4", 64, NOMEM(4)},
   };
   const int rounds = argc > 3 ? atoi(argv[3]) : 2;
   for (int round = 0; round < rounds; ++round)
