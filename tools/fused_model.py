@@ -14,8 +14,13 @@ launch time (rNN_*_kernel_steady.csv), and sets three times side by side:
   lds    SQ_LDS_IDX_ACTIVE cycles / CUs at the shader clock, and the same
          without SQ_LDS_BANK_CONFLICT — the LDS time a conflict-free table
          layout with the SAME instruction count would take;
-  hbm    algorithmic bytes at the copy ceiling (a plain nt 16-B-per-lane copy,
-         MI355X_MICROARCH.md / bench.py copy_ceiling: 6.29-6.48 TB/s).
+  hbm    algorithmic bytes at the kernel's own memory skeleton (DESIGN §3,
+         "the memory skeleton"): a read-only pass (the checksum-only kernels)
+         at the read-only skeleton, 0.9236 of 8 TB/s; a pass that reads k
+         shards and writes p (the fused kernels) at the C2 encode skeleton,
+         0.7807 of 8 TB/s. (Round 5 priced every kernel at the 1:1 copy
+         ceiling, 6.29 TB/s, which made a read-only kernel look closer to its
+         bound than it is.)
 
 The kernel cannot run faster than max(valu, lds, hbm); `overlap` is that
 bound over the measured time. A formulation is worth building when the bound
@@ -34,6 +39,15 @@ P = lambda *a: os.path.join(ROOT, "profiles", *a)  # noqa: E731
 CUS = 256
 CLOCK_GHZ = 2.4          # MI355X shader clock (MI355X_MICROARCH.md)
 COPY_CEILING = 6.29e12   # B/s, nt float4 copy (MI355X_MICROARCH.md; bench.py copy probe 6.29-6.48)
+# per-kernel HBM ceilings: the memory skeletons (profiles/r05/r05_skel_probe_m.jsonl)
+READ_ONLY_SKELETON = 0.9236 * 8e12   # pq_check-shaped read-only pass
+ENCODE_SKELETON = 0.7807 * 8e12      # C2 k10p4: 10 shards read, 4 written
+READ_ONLY_KERNELS = ("crc64_shards_pre", "crc32c_shards_pre", "crc64_pre_", "ec_verify")
+
+
+def hbm_ceiling(label):
+    """B/s the kernel's memory pattern reaches with no arithmetic."""
+    return READ_ONLY_SKELETON if any(k in label for k in READ_ONLY_KERNELS) else ENCODE_SKELETON
 TARGET_MS = 2.9          # VERDICT r04: encode + CRC64 at C2 <= 2.9 ms (0.648 of 8 TB/s)
 
 
@@ -85,7 +99,7 @@ def row(label, c, meas_ms, nbytes, rate):
     conf = c.get("SQ_LDS_BANK_CONFLICT", 0)
     lds_ms = act / CUS / CLOCK_GHZ / 1e6
     lds_cf_ms = (act - conf) / CUS / CLOCK_GHZ / 1e6
-    hbm_ms = nbytes / COPY_CEILING * 1e3
+    hbm_ms = nbytes / hbm_ceiling(label) * 1e3
     bound = max(valu_ms, lds_ms, hbm_ms)
     bound_cf = max(valu_ms, lds_cf_ms, hbm_ms)
     ov = f"{bound / meas_ms:.3f}" if meas_ms == meas_ms else ""
@@ -110,7 +124,8 @@ def main(argv):
     counters = sections(a.counters)
     print(f"# fused-kernel resource model: tools/fused_model.py {' '.join(argv[1:])}")
     print(f"# VALU issue rate {rate:.3f} wave-instr/CU/ns (profiles/r03/r03_valu_probe.jsonl, 4 waves/SIMD); "
-          f"{CUS} CUs at {CLOCK_GHZ} GHz; HBM at the copy ceiling {COPY_CEILING / 1e12:.2f} TB/s; "
+          f"{CUS} CUs at {CLOCK_GHZ} GHz; HBM at each kernel's memory skeleton (read-only "
+          f"{READ_ONLY_SKELETON / 1e12:.2f} TB/s, encode {ENCODE_SKELETON / 1e12:.2f} TB/s); "
           f"{a.bytes / 1e9:.3f} GB per launch")
     print("kernel,valu_ms,lds_ms,lds_conflict_free_ms,hbm_ms,bound_ms,bound_conflict_free_ms,measured_ms,"
           "bound_over_measured,conflict_share")
