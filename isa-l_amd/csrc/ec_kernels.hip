@@ -593,6 +593,128 @@ __global__ __launch_bounds__(kBlock) void ec_update_b1(const uint64_t* __restric
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Wide passes with the products looked up in LDS (ec_encode_ldsx, round 6)
+//
+// The v_perm product costs ~4.5 VALU per (source dword, output row), so passes
+// of 6-8 rows are VALU-bound ("the memory skeleton"). Here one LDS
+// lookup returns the products of one source-byte field with ALL P
+// coefficients of the pass: per source j a 32-entry table T5_j (bits 0-4 of
+// the byte) and an 8-entry table T3_j (bits 5-7), 8-byte entries whose byte l
+// is row l's product (isal_hip_build_ldsx_tables). A lane keeps its 16 byte
+// positions as 16 two-dword accumulators (byte l = row l's partial) —
+// two lookups and one XOR3 per half per source byte — and transposes them
+// into the P rows with v_perm once per tile. Per source dword: 12 offset ops
+// (the fields pre-scaled by 8, one SDWA add of the table base each), 8 XOR3
+// and 8 ds_read_b64, whatever P. Both tables fill at most one LDS bank row
+// (32 x 8 B), so the lookups never bank-conflict.
+// ---------------------------------------------------------------------------
+struct Acc64 {
+  uint32_t lo, hi;
+};
+
+template <int B>
+__device__ __forceinline__ uint32_t add_byte(uint32_t v, uint32_t base) {
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+        : "=v"(r) : "v"(v), "v"(base));
+  else if constexpr (B == 1)
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+        : "=v"(r) : "v"(v), "v"(base));
+  else if constexpr (B == 2)
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+        : "=v"(r) : "v"(v), "v"(base));
+  else
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+        : "=v"(r) : "v"(v), "v"(base));
+  return r;
+}
+
+__device__ __forceinline__ uint64_t lds_u64(uint32_t addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint64_t*>(static_cast<uintptr_t>(addr));
+}
+
+// acc[4d + b] ^= T5[bits 0-4 of byte b of dword d] ^ T3[bits 5-7] for one
+// 16-byte source chunk; b5 / b3: LDS byte addresses of the source's tables
+__device__ __forceinline__ void ldsx_acc(Acc64 (&acc)[16], const uint4& x, uint32_t b5, uint32_t b3) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t lo8 = (w[d] << 3) & 0xF8F8F8F8u;  // bits 0-4 of each byte, times 8
+    const uint32_t hi8 = (w[d] >> 2) & 0x38383838u;  // bits 5-7 of each byte, times 8
+    auto one = [&](auto bc) __attribute__((always_inline)) {
+      constexpr int b = decltype(bc)::value;
+      const uint64_t p = lds_u64(add_byte<b>(lo8, b5));
+      const uint64_t q = lds_u64(add_byte<b>(hi8, b3));
+      Acc64& a = acc[4 * d + b];
+      a.lo = xor3(a.lo, static_cast<uint32_t>(p), static_cast<uint32_t>(q));
+      a.hi = xor3(a.hi, static_cast<uint32_t>(p >> 32), static_cast<uint32_t>(q >> 32));
+    };
+    one(std::integral_constant<int, 0>{});
+    one(std::integral_constant<int, 1>{});
+    one(std::integral_constant<int, 2>{});
+    one(std::integral_constant<int, 3>{});
+  }
+}
+
+template <int P, int U>
+__global__ __launch_bounds__(kBlock) void ec_encode_ldsx(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
+                                                         int dst0, const uint32_t* __restrict__ tbl,
+                                                         const uint64_t* __restrict__ ltg, int len, int k,
+                                                         unsigned nitems, unsigned tiles) {
+  extern __shared__ uint64_t ldsx_t[];  // [k][32] T5, then [k][8] T3
+  for (int i = threadIdx.x; i < k * ISAL_HIP_LDSX_ENTRIES; i += kBlock) ldsx_t[i] = ltg[i];
+  __syncthreads();
+  const uint32_t base5 = lds_off(ldsx_t), base3 = base5 + static_cast<uint32_t>(k) * 256u;
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned v = xcd_item(w, nitems, 1);
+    const unsigned stripe = v / tiles;
+    const unsigned tile = v - stripe * tiles;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
+    const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
+    if (off + kVec > len) {
+      if (off < len) dot_bytes<P>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off));
+      continue;
+    }
+    Acc64 acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = Acc64{0u, 0u};
+    int j = 0;
+    for (; j + U <= k; j += U) {
+      uint4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = load16<kBufNT>(sp[src0 + j + u], off, len);
+#pragma unroll
+      for (int u = 0; u < U; ++u) ldsx_acc(acc, x[u], base5 + (j + u) * 256u, base3 + (j + u) * 64u);
+    }
+    for (; j < k; ++j)
+      ldsx_acc(acc, load16<kBufNT>(sp[src0 + j], off, len), base5 + j * 256u, base3 + j * 64u);
+    // transpose: row l, dword d = byte l of acc[4d .. 4d + 3] (rows 0-3 in .lo, 4-7 in .hi)
+    uint32_t out[P][4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (4 * h >= P) continue;
+        const uint32_t A = h ? acc[4 * d].hi : acc[4 * d].lo, B = h ? acc[4 * d + 1].hi : acc[4 * d + 1].lo;
+        const uint32_t C = h ? acc[4 * d + 2].hi : acc[4 * d + 2].lo, D = h ? acc[4 * d + 3].hi : acc[4 * d + 3].lo;
+        const uint32_t ab0 = __builtin_amdgcn_perm(B, A, 0x05010400u), ab1 = __builtin_amdgcn_perm(B, A, 0x07030602u);
+        const uint32_t cd0 = __builtin_amdgcn_perm(D, C, 0x05010400u), cd1 = __builtin_amdgcn_perm(D, C, 0x07030602u);
+        const uint32_t r[4] = {__builtin_amdgcn_perm(cd0, ab0, 0x05040100u), __builtin_amdgcn_perm(cd0, ab0, 0x07060302u),
+                               __builtin_amdgcn_perm(cd1, ab1, 0x05040100u), __builtin_amdgcn_perm(cd1, ab1, 0x07060302u)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (4 * h + q < P) out[4 * h + q][d] = r[q];
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < P; ++l)
+      store16<kBufNT>(sp[dst0 + l], off, make_uint4(out[l][0], out[l][1], out[l][2], out[l][3]), len);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launch helpers
 // ---------------------------------------------------------------------------
@@ -736,15 +858,49 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
     launch_fl<P, U, kEncLUT>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
 }
 
+// Passes of 7-8 rows over at most kLdsxMaxK sources take the LDS product
+// tables (ec_encode_ldsx) when the caller uploaded them (isal_hip_encmask.ldsx;
+// ISAL_HIP_ENC_LDSX=1: every pass of 5-8 rows, =0 off). Against
+// ec_encode_glds, ms per launch: bench.py batch encode k20 p8 1.38 vs 1.57,
+// k16 p8 2.23 vs 2.46, k10 p8 3.08 vs 3.26, k10 p7 3.01 vs 3.05, same box
+// (profiles/r06/r06_wide_ldsx_bench_ab_b.jsonl). Below 7 rows it does not pay
+// in the library: k20 p6 1.30 vs 1.29 there (the standalone sweep,
+// r06_wide_ldsx_probe_b.jsonl, had it 5 % ahead on another layout), k10 p6
+// and k10 p4 within 1 %, k20 p4 3 % behind.
+constexpr int kLdsxRows = 5, kLdsxAutoRows = 7, kLdsxMaxK = 64;
+bool enc_ldsx(int P, int k, const uint64_t* ldsx) {
+  if (!ldsx || P < kLdsxRows || k > kLdsxMaxK) return false;
+  const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_LDSX);
+  if (v == 0 || v == 1) return v == 1;
+  return P >= kLdsxAutoRows;
+}
+
+// Sources loaded together by ec_encode_ldsx: 2 (the same sweep: 2-4 within 1 %
+// of each other, 1 and 5 up to 5 % slower — more loads in flight cost VGPRs,
+// and the lane already has 32 accumulator VGPRs live).
+constexpr int kLdsxGroup = 2;
+
+template <int P, int U>
+void launch_ldsx(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
+                 const uint32_t* tbl, const uint64_t* ldsx, int len, int k, unsigned nitems, unsigned tiles) {
+  if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2) fprintf(stderr, "isal_hip: kernel ec_encode_ldsx<%d, %d>\n", P, U);
+  ISAL_LAUNCH((ec_encode_ldsx<P, U>), dim3(grid), dim3(kBlock), static_cast<size_t>(k) * ISAL_HIP_LDSX_ENTRIES * 8, s,
+              ptrs, ptr_stride, src0, dst0, tbl, ldsx, len, k, nitems, tiles);
+}
+
 template <int P>
 hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0, const uint32_t* tbl,
-                       int len, int k, unsigned nstripes, bool vec16, bool x, unsigned long long r0m,
-                       unsigned c0m, hipStream_t s) {
+                       const uint64_t* ldsx, int len, int k, unsigned nstripes, bool vec16, bool x,
+                       unsigned long long r0m, unsigned c0m, hipStream_t s) {
   const unsigned span = vec16 ? kTile : kBlock;
   const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + span - 1) / span);
   const unsigned nitems = nstripes * tiles;
   const unsigned grid = grid_for(nitems);
-  if (vec16 && enc_glds(P)) {
+  if (vec16 && enc_ldsx(P, k, ldsx)) {
+    if constexpr (P >= kLdsxRows) {
+      launch_ldsx<P, kLdsxGroup>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, ldsx, len, k, nitems, tiles);
+    }
+  } else if (vec16 && enc_glds(P)) {
     launch_glds_r<P>(x, grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
   } else if (vec16) {
     switch (enc_group(k, P)) {
@@ -804,6 +960,7 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
                                       void* stream) {
   if (len <= 0 || rows <= 0 || nstripes <= 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint64_t* ldsx_all = em ? em->ldsx : nullptr;
   em = enc_xor_masks(em);
   const unsigned per = stripes_per_launch(len, vec16 != 0);
   for (long long s0 = 0; s0 < nstripes; s0 += per) {
@@ -812,6 +969,8 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
     for (int r0 = 0; r0 < rows; r0 += EC_MAX_ROWS_PER_PASS) {
       const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
       const uint32_t* tbl = d_tbl + static_cast<size_t>(kTbl) * k * r0;
+      const uint64_t* ldsx =
+          ldsx_all ? ldsx_all + static_cast<size_t>(r0 / EC_MAX_ROWS_PER_PASS) * k * ISAL_HIP_LDSX_ENTRIES : nullptr;
       const int dst0 = dst_idx0 + r0;
       const int g = r0 / EC_MAX_ROWS_PER_PASS;
       const bool x = em && g < EC_MAX_PASSES && ((em->ok >> g) & 1u);
@@ -821,7 +980,7 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
       switch (P) {
 #define EC_CASE(n)                                                                                      \
   case n:                                                                                               \
-    e = encode_pass<n>(ptrs, ptr_stride, src_idx0, dst0, tbl, len, k, ns, vec16 != 0, x, r0m, c0m, s); \
+    e = encode_pass<n>(ptrs, ptr_stride, src_idx0, dst0, tbl, ldsx, len, k, ns, vec16 != 0, x, r0m, c0m, s); \
     break;
         EC_CASE(1) EC_CASE(2) EC_CASE(3) EC_CASE(4) EC_CASE(5) EC_CASE(6) EC_CASE(7) EC_CASE(8)
 #undef EC_CASE

@@ -229,6 +229,35 @@ isal_hip_build_tables(int k, int rows, const unsigned char *gftbls, uint32_t *tb
         }
 }
 
+/* LDS product tables of the wide passes (layout: isal_hip_internal.h). */
+size_t
+isal_hip_ldsx_words(int k, int rows)
+{
+        const int passes = (rows + EC_MAX_ROWS_PER_PASS - 1) / EC_MAX_ROWS_PER_PASS;
+        return (size_t) passes * (size_t) k * ISAL_HIP_LDSX_ENTRIES;
+}
+
+void
+isal_hip_build_ldsx_tables(int k, int rows, const unsigned char *gftbls, uint64_t *out)
+{
+        int r0, j, l, v;
+        for (r0 = 0; r0 < rows; r0 += EC_MAX_ROWS_PER_PASS) {
+                const int P = rows - r0 < EC_MAX_ROWS_PER_PASS ? rows - r0 : EC_MAX_ROWS_PER_PASS;
+                uint64_t *t5 = out + (size_t) (r0 / EC_MAX_ROWS_PER_PASS) * k * ISAL_HIP_LDSX_ENTRIES,
+                         *t3 = t5 + (size_t) k * 32;
+                memset(t5, 0, (size_t) k * ISAL_HIP_LDSX_ENTRIES * 8);
+                for (j = 0; j < k; j++)
+                        for (l = 0; l < P; l++) {
+                                const unsigned char c = gftbls[((size_t) (r0 + l) * k + j) * 32 + 1];
+                                for (v = 0; v < 32; v++)
+                                        t5[(size_t) j * 32 + v] |= (uint64_t) gf_mul(c, (unsigned char) v) << (8 * l);
+                                for (v = 0; v < 8; v++)
+                                        t3[(size_t) j * 8 + v] |= (uint64_t) gf_mul(c, (unsigned char) (v << 5))
+                                                                  << (8 * l);
+                        }
+        }
+}
+
 void
 isal_hip_xor_rows(int k, int rows, const unsigned char *gftbls, isal_hip_xrows *x)
 {

@@ -54,8 +54,23 @@ typedef struct {
         unsigned ok;
         unsigned c0[EC_MAX_PASSES];
         unsigned long long r0[EC_MAX_PASSES];
+        /* device copy of isal_hip_build_ldsx_tables' output, or NULL: the
+         * wide passes may then look their products up in LDS (ec_kernels.hip
+         * ec_encode_ldsx). isal_hip_enc_masks leaves it NULL; a caller that
+         * uploads the tables sets it. */
+        const uint64_t *ldsx;
 } isal_hip_encmask;
 void isal_hip_enc_masks(int k, int rows, const unsigned char *gftbls, isal_hip_encmask *m);
+
+/* LDS product tables of a pass of P <= 8 rows: for each source j, a 32-entry
+ * table T5_j[v] (8 bytes, byte l = c[r0 + l][j] * v: bits 0-4 of a source
+ * byte) and an 8-entry table T3_j[v] (byte l = c[r0 + l][j] * (v << 5): bits
+ * 5-7); pass g occupies k * ISAL_HIP_LDSX_ENTRIES words: [k][32] T5, then
+ * [k][8] T3. A source byte's products with all P coefficients are two
+ * lookups (T5 ^ T3). */
+#define ISAL_HIP_LDSX_ENTRIES 40
+size_t isal_hip_ldsx_words(int k, int rows);
+void isal_hip_build_ldsx_tables(int k, int rows, const unsigned char *gftbls, uint64_t *out);
 
 /* Kernel launchers (ec_kernels.hip). Return 0 or a hipError_t value.
  * `stream` is a hipStream_t. `vec16` = every shard address is 16-byte aligned. */
@@ -198,6 +213,7 @@ enum {
         ISAL_HIP_KNOB_ENC_GROUP,     /* 12/10/8/6/5/4: encode load group forced (tests: every group path) */
         ISAL_HIP_KNOB_KARG_NARROW,   /* drop-in kernel-argument encode with 4-byte lanes: 1 on, 0 off */
         ISAL_HIP_KNOB_ENC_WIDE5,     /* 0: 6-8 row passes keep the largest load group (no groups of 5) */
+        ISAL_HIP_KNOB_ENC_LDSX,      /* 0: wide passes compute products with v_perm, not LDS product tables */
         ISAL_HIP_KNOB_COUNT
 };
 long long isal_hip_knob(int id);

@@ -50,6 +50,7 @@ static const knob_def defs[ISAL_HIP_KNOB_COUNT] = {
         [ISAL_HIP_KNOB_ENC_GROUP] = {"ISAL_HIP_ENC_GROUP", NULL},
         [ISAL_HIP_KNOB_KARG_NARROW] = {"ISAL_HIP_KARG_NARROW", NULL},
         [ISAL_HIP_KNOB_ENC_WIDE5] = {"ISAL_HIP_ENC_WIDE5", NULL},
+        [ISAL_HIP_KNOB_ENC_LDSX] = {"ISAL_HIP_ENC_LDSX", NULL},
 };
 
 static long long values[ISAL_HIP_KNOB_COUNT];

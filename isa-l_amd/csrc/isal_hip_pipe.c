@@ -32,6 +32,7 @@ struct isal_hip_pipe {
         unsigned char *d_buf; /* depth x (k + rows) x len */
         uint64_t *d_ptrs;     /* depth x (k + rows) */
         uint32_t *d_tbl;
+        uint64_t *d_ldsx;      /* LDS product tables of the wide passes (NULL: not used) */
         isal_hip_encmask em;   /* 0/1 rows and columns of the coefficients */
         hipEvent_t *src_ready; /* depth x k */
         hipEvent_t *parity_done, *slot_free;
@@ -112,6 +113,20 @@ isal_hip_pipe_create(isal_hip_pipe **out, int len, int k, int rows, const unsign
                 if (hipMemcpy(p->d_ptrs, h_ptrs, nptr * 8, hipMemcpyHostToDevice) != hipSuccess ||
                     hipMemcpy(p->d_tbl, h_tbl, ntbl * 4, hipMemcpyHostToDevice) != hipSuccess)
                         rc = ISAL_HIP_EHIP;
+        }
+        if (rc == ISAL_HIP_OK && mode == ISAL_HIP_PIPE_ENCODE && k <= 64 && rows >= 5) {
+                /* the wide passes' LDS product tables (ec_encode_ldsx) */
+                const size_t nw = isal_hip_ldsx_words(k, rows);
+                uint64_t *hx = (uint64_t *) malloc(nw * 8);
+                if (!hx || hipMalloc((void **) &p->d_ldsx, nw * 8) != hipSuccess)
+                        rc = hx ? ISAL_HIP_EHIP : ISAL_HIP_ENOMEM;
+                if (rc == ISAL_HIP_OK) {
+                        isal_hip_build_ldsx_tables(k, rows, gftbls, hx);
+                        if (hipMemcpy(p->d_ldsx, hx, nw * 8, hipMemcpyHostToDevice) != hipSuccess)
+                                rc = ISAL_HIP_EHIP;
+                        p->em.ldsx = p->d_ldsx;
+                }
+                free(hx);
         }
         free(h_ptrs);
         free(h_tbl);
@@ -227,6 +242,8 @@ isal_hip_pipe_destroy(isal_hip_pipe *p)
                 (void) hipFree(p->d_ptrs);
         if (p->d_tbl)
                 (void) hipFree(p->d_tbl);
+        if (p->d_ldsx)
+                (void) hipFree(p->d_ldsx);
         free(p->src_ready);
         free(p->parity_done);
         free(p->slot_free);

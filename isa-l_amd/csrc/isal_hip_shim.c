@@ -2045,6 +2045,7 @@ struct isal_hip_batch {
         isal_hip_encmask em; /* 0/1 rows and columns: XORs instead of lookups */
         /* CRC32C state, allocated on first use: kernel tables + combine plan,
          * and the per-lane partials (crc_kernels.hip) */
+        uint64_t *d_ldsx; /* LDS product tables of the wide passes (NULL: not used) */
         isal_hip_crc_geom crc;
         uint32_t *d_crc, *d_part, *d_tail;
         /* CRC64 state, allocated on first use: one table set per variant
@@ -2194,10 +2195,24 @@ batch_set_tables_impl(isal_hip_batch *b, const unsigned char *gftbls)
         if (e == hipSuccess)
                 e = hipMemcpy(b->d_tbl, h, n * 4, hipMemcpyHostToDevice);
         free(h);
+        /* the wide passes' LDS product tables (ec_encode_ldsx): k <= 64, a
+         * pass of at least 5 rows */
+        if (e == hipSuccess && b->k >= 1 && b->k <= 64 && b->rows >= 5) {
+                const size_t nw = isal_hip_ldsx_words(b->k, b->rows);
+                uint64_t *hx = (uint64_t *) malloc(nw * 8);
+                if (!hx)
+                        return ISAL_HIP_ENOMEM;
+                isal_hip_build_ldsx_tables(b->k, b->rows, gftbls, hx);
+                if (!b->d_ldsx && hipMalloc((void **) &b->d_ldsx, nw * 8) != hipSuccess)
+                        b->d_ldsx = NULL;
+                e = b->d_ldsx ? hipMemcpy(b->d_ldsx, hx, nw * 8, hipMemcpyHostToDevice) : hipSuccess;
+                free(hx);
+        }
         if (e != hipSuccess)
                 return ISAL_HIP_EHIP;
         b->xr = xr;
         b->em = em;
+        b->em.ldsx = b->d_ldsx;
         return ISAL_HIP_OK;
 }
 
@@ -2243,6 +2258,8 @@ isal_hip_batch_destroy(isal_hip_batch *b)
                 (void) hipFree(b->d_ptrs);
         if (b->d_tbl)
                 (void) hipFree(b->d_tbl);
+        if (b->d_ldsx)
+                (void) hipFree(b->d_ldsx);
         if (b->d_crc)
                 (void) hipFree(b->d_crc);
         if (b->d_part)

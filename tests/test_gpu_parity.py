@@ -366,8 +366,9 @@ def _coef_01(rng, k, rows, kind):
     return c.reshape(-1)
 
 
-@pytest.mark.parametrize("xor,lds,glds", [("1", "1", "1"), ("0", "1", "1"), ("1", "1", "0"), ("0", "1", "0"),
-                                          ("1", "0", "0"), ("0", "0", "0")])
+@pytest.mark.parametrize("xor,lds,glds,ldsx", [("1", "1", "1", "0"), ("0", "1", "1", "0"), ("1", "1", "0", "0"),
+                                               ("0", "1", "0", "0"), ("1", "0", "0", "0"), ("0", "0", "0", "0"),
+                                               ("1", "1", "1", "1"), ("0", "0", "0", "1")])
 @pytest.mark.parametrize("k,rows,n,ns,gen", [
     (10, 4, 65536 + 48, 9, "rs"),       # C2 shape class, pairs of sources
     (10, 6, 65536, 8, "rs"),            # P = 6: no pairs
@@ -382,18 +383,20 @@ def _coef_01(rng, k, rows, kind):
     (10, 4, 65536, 5, "mask"), (20, 6, 16384, 3, "mask"), (10, 8, 8192, 3, "mask"),
     (10, 5, 8192, 3, "rowonly"), (10, 4, 8192, 3, "big"),
 ])
-def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, lds, glds, k, rows, n, ns, gen):
+def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, lds, glds, ldsx, k, rows, n, ns, gen):
     """Rows and columns of 0/1 coefficients (gf_gen_rs_matrix row 0 and column
     0, RAID P) take XORs instead of v_perm lookups (ISAL_HIP_ENC_XOR), the low
     table halves come from LDS (ISAL_HIP_ENC_LDS) and passes of 5-8 rows stage
     their sources through the LDS-DMA ring (ISAL_HIP_ENC_GLDS, which always
-    takes the LDS halves), all default on: batch and drop-in encode == oracle
-    with each on and off."""
+    takes the LDS halves) — or, for batches over k <= 64 sources, look their
+    products up in LDS product tables (ISAL_HIP_ENC_LDSX=1 forces them for
+    every such pass): batch and drop-in encode == oracle with each on and off."""
     import torch
 
     _setenv(monkeypatch, "ISAL_HIP_ENC_XOR", xor)
     _setenv(monkeypatch, "ISAL_HIP_ENC_LDS", lds)
     _setenv(monkeypatch, "ISAL_HIP_ENC_GLDS", glds)
+    _setenv(monkeypatch, "ISAL_HIP_ENC_LDSX", ldsx)
     if gen == "rs":
         coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
     else:
@@ -428,15 +431,17 @@ def test_encode_xor_fast_path_vs_oracle(engine, oracle, gpu, monkeypatch, xor, l
     (13, 6, 4096 * 5, 3, "rs"),         # odd k: the LDS-DMA ring's single last source
     (9, 7, 4096 * 4 + 16, 3, "mask"),   # ring of 4 over k = 9: a partial last round
 ])
-@pytest.mark.parametrize("glds", ["1", "0"])
-def test_encode_load_groups_vs_oracle(engine, oracle, gpu, monkeypatch, glds, k, rows, n, ns, gen):
+@pytest.mark.parametrize("glds,ldsx", [("1", "0"), ("0", "0"), ("1", "1"), (None, None)])
+def test_encode_load_groups_vs_oracle(engine, oracle, gpu, monkeypatch, glds, ldsx, k, rows, n, ns, gen):
     """Stripes of two or more load groups (enc_group: k a multiple of 8, 10 or
     12 above it): batch encode == oracle with ragged tails, odd group counts
-    and two passes; passes of 5-8 rows through the LDS-DMA ring (default) and
-    through registers (ISAL_HIP_ENC_GLDS=0)."""
+    and two passes; passes of 5-8 rows through the LDS product tables
+    (ISAL_HIP_ENC_LDSX=1), the LDS-DMA ring (ISAL_HIP_ENC_LDSX=0), through
+    registers (ISAL_HIP_ENC_GLDS=0) and as the library picks by default."""
     import torch
 
     _setenv(monkeypatch, "ISAL_HIP_ENC_GLDS", glds)
+    _setenv(monkeypatch, "ISAL_HIP_ENC_LDSX", ldsx)
 
     if gen == "rs":
         coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
@@ -1835,13 +1840,17 @@ def test_bench_rccl_control_plane_single_rank(gpu):
 
 @pytest.mark.parametrize("args,env", [
     (["--k", "10", "--p", "4"], {}),                                  # C2 shape: XOR path, groups of 10
-    (["--k", "10", "--p", "8"], {}),                                  # 8 rows: the LDS-DMA ring
-    (["--k", "20", "--p", "6", "--len", "262144", "--stripes", "8"], {}),
-    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_WIDE5": "0", "ISAL_HIP_ENC_GLDS": "0"}),
-    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_LDS": "0", "ISAL_HIP_ENC_XOR": "0", "ISAL_HIP_ENC_GLDS": "0"}),
-    (["--k", "12", "--p", "5"], {"ISAL_HIP_ENC_GROUP": "4", "ISAL_HIP_ENC_GLDS": "0"}),
-    (["--k", "10", "--p", "8"], {"ISAL_HIP_ENC_GLDS": "0"}),         # 8 rows through registers
-    (["--k", "7", "--p", "5"], {"ISAL_HIP_ENC_XOR": "0"}),            # LDS-DMA ring, lookups only
+    (["--k", "10", "--p", "8"], {}),                                  # 8 rows: LDS product tables
+    (["--k", "20", "--p", "7", "--len", "262144", "--stripes", "8"], {}),  # 7 rows: product tables
+    (["--k", "20", "--p", "6", "--len", "262144", "--stripes", "8"], {}),  # 6 rows: the LDS-DMA ring
+    (["--k", "7", "--p", "5"], {"ISAL_HIP_ENC_LDSX": "1"}),           # product tables forced, odd k
+    (["--k", "10", "--p", "8"], {"ISAL_HIP_ENC_LDSX": "0"}),          # 8 rows: the LDS-DMA ring
+    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_WIDE5": "0", "ISAL_HIP_ENC_GLDS": "0", "ISAL_HIP_ENC_LDSX": "0"}),
+    (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_LDS": "0", "ISAL_HIP_ENC_XOR": "0", "ISAL_HIP_ENC_GLDS": "0",
+                                 "ISAL_HIP_ENC_LDSX": "0"}),
+    (["--k", "12", "--p", "5"], {"ISAL_HIP_ENC_GROUP": "4", "ISAL_HIP_ENC_GLDS": "0", "ISAL_HIP_ENC_LDSX": "0"}),
+    (["--k", "10", "--p", "8"], {"ISAL_HIP_ENC_GLDS": "0", "ISAL_HIP_ENC_LDSX": "0"}),  # 8 rows through registers
+    (["--k", "7", "--p", "5"], {"ISAL_HIP_ENC_XOR": "0", "ISAL_HIP_ENC_LDSX": "0"}),     # LDS-DMA ring, lookups only
     (["--workload", "decode"], {}),
 ])
 def test_bench_kernel_label_matches_launch(gpu, args, env):

@@ -169,7 +169,9 @@ static void ldsx(int P, int U, unsigned grid, const uint64_t* dp, int stride, co
                  unsigned nitems, unsigned tiles) {
 #define L(p, u) \
   if (P == p && U == u) return launch_ldsx<p, u>(grid, dp, stride, dlt, len, k, nitems, tiles);
-  L(4, 5) L(6, 5) L(8, 5) L(4, 10) L(6, 10) L(8, 10) L(6, 4) L(8, 4) L(8, 2) L(6, 2)
+#define LU(p) L(p, 1) L(p, 2) L(p, 3) L(p, 4) L(p, 5)
+  LU(3) LU(4) LU(5) LU(6) LU(7) LU(8)
+#undef LU
 #undef L
   fprintf(stderr, "no instantiation P=%d U=%d\n", P, U);
   exit(1);
@@ -178,8 +180,11 @@ static void ldsx(int P, int U, unsigned grid, const uint64_t* dp, int stride, co
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 10;
   const int rounds = argc > 2 ? atoi(argv[2]) : 2;
-  const Shape shapes[] = {{20, 8, 4 << 20, 64}, {20, 6, 4 << 20, 64}, {10, 8, 1 << 20, 1024}, {10, 6, 1 << 20, 1024},
-                          {10, 4, 1 << 20, 1024}};
+  const Shape shapes[] = {{10, 4, 1 << 20, 1024}, {10, 3, 1 << 20, 1024}, {10, 5, 1 << 20, 1024},
+                          {10, 6, 1 << 20, 1024}, {10, 7, 1 << 20, 1024}, {10, 8, 1 << 20, 1024},
+                          {20, 4, 4 << 20, 64},    {20, 5, 4 << 20, 64},    {20, 6, 4 << 20, 64},
+                          {20, 7, 4 << 20, 64},    {20, 8, 4 << 20, 64},    {8, 6, 1 << 20, 1024},
+                          {16, 8, 1 << 20, 512},   {12, 4, 1 << 20, 1024}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -232,12 +237,9 @@ int main(int argc, char** argv) {
         int U;
         unsigned grid;
       };
-      const Var vars[] = {{"lib", 0, 0},           {"ldsx_u5", 5, nitems},      {"ldsx_u10", 10, nitems},
-                          {"ldsx_u4", 4, nitems},   {"ldsx_u2", 2, nitems},      {"ldsx_u5_g8k", 5, 8192},
-                          {"ldsx_u5_g16k", 5, 16384}};
+      const Var vars[] = {{"lib", 0, 0},         {"ldsx_u1", 1, nitems}, {"ldsx_u2", 2, nitems},
+                          {"ldsx_u3", 3, nitems}, {"ldsx_u4", 4, nitems}, {"ldsx_u5", 5, nitems}};
       for (const Var& var : vars) {
-        if (var.U && !((p == 4 || p == 6 || p == 8) && ((var.U == 5 || var.U == 10) || (var.U == 4 || var.U == 2) && p >= 6)))
-          continue;
         auto go = [&]() {
           if (!var.U)
             CK(static_cast<hipError_t>(isal_hip_launch_encode(dp, stride, 0, k, dt, len, k, p, ns, 1, &em, nullptr)));
