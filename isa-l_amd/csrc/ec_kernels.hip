@@ -659,6 +659,33 @@ __device__ __forceinline__ void ldsx_acc(Acc64 (&acc)[16], const uint4& x, uint3
   }
 }
 
+// transpose the 16 accumulators into the P rows' 16 bytes and store them: row
+// l, dword d = byte l of acc[4d .. 4d + 3] (rows 0-3 in .lo, 4-7 in .hi)
+template <int P>
+__device__ __forceinline__ void ldsx_store(const Acc64 (&acc)[16], const uint64_t* __restrict__ sp, int dst0,
+                                           long long off, int len) {
+  uint32_t out[P][4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (4 * h >= P) continue;
+      const uint32_t A = h ? acc[4 * d].hi : acc[4 * d].lo, B = h ? acc[4 * d + 1].hi : acc[4 * d + 1].lo;
+      const uint32_t C = h ? acc[4 * d + 2].hi : acc[4 * d + 2].lo, D = h ? acc[4 * d + 3].hi : acc[4 * d + 3].lo;
+      const uint32_t ab0 = __builtin_amdgcn_perm(B, A, 0x05010400u), ab1 = __builtin_amdgcn_perm(B, A, 0x07030602u);
+      const uint32_t cd0 = __builtin_amdgcn_perm(D, C, 0x05010400u), cd1 = __builtin_amdgcn_perm(D, C, 0x07030602u);
+      const uint32_t r[4] = {__builtin_amdgcn_perm(cd0, ab0, 0x05040100u), __builtin_amdgcn_perm(cd0, ab0, 0x07060302u),
+                             __builtin_amdgcn_perm(cd1, ab1, 0x05040100u), __builtin_amdgcn_perm(cd1, ab1, 0x07060302u)};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * h + q < P) out[4 * h + q][d] = r[q];
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < P; ++l)
+    store16<kBufNT>(sp[dst0 + l], off, make_uint4(out[l][0], out[l][1], out[l][2], out[l][3]), len);
+}
+
 template <int P, int U>
 __global__ __launch_bounds__(kBlock) void ec_encode_ldsx(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
                                                          int dst0, const uint32_t* __restrict__ tbl,
@@ -681,37 +708,24 @@ __global__ __launch_bounds__(kBlock) void ec_encode_ldsx(const uint64_t* __restr
     Acc64 acc[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = Acc64{0u, 0u};
-    int j = 0;
-    for (; j + U <= k; j += U) {
-      uint4 x[U];
+    // groups of U sources, double-buffered: group g + 1's loads are issued
+    // before group g is folded (2U loads in flight per lane); k is uniform,
+    // so the bounds tests are scalar branches
+    uint4 a[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) x[u] = load16<kBufNT>(sp[src0 + j + u], off, len);
+    for (int u = 0; u < U; ++u) a[u] = u < k ? load16<kBufNT>(sp[src0 + u], off, len) : make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < k; j += U) {
+      uint4 b[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) ldsx_acc(acc, x[u], base5 + (j + u) * 256u, base3 + (j + u) * 64u);
+      for (int u = 0; u < U; ++u)
+        b[u] = j + U + u < k ? load16<kBufNT>(sp[src0 + j + U + u], off, len) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j + u < k) ldsx_acc(acc, a[u], base5 + (j + u) * 256u, base3 + (j + u) * 64u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = b[u];
     }
-    for (; j < k; ++j)
-      ldsx_acc(acc, load16<kBufNT>(sp[src0 + j], off, len), base5 + j * 256u, base3 + j * 64u);
-    // transpose: row l, dword d = byte l of acc[4d .. 4d + 3] (rows 0-3 in .lo, 4-7 in .hi)
-    uint32_t out[P][4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (4 * h >= P) continue;
-        const uint32_t A = h ? acc[4 * d].hi : acc[4 * d].lo, B = h ? acc[4 * d + 1].hi : acc[4 * d + 1].lo;
-        const uint32_t C = h ? acc[4 * d + 2].hi : acc[4 * d + 2].lo, D = h ? acc[4 * d + 3].hi : acc[4 * d + 3].lo;
-        const uint32_t ab0 = __builtin_amdgcn_perm(B, A, 0x05010400u), ab1 = __builtin_amdgcn_perm(B, A, 0x07030602u);
-        const uint32_t cd0 = __builtin_amdgcn_perm(D, C, 0x05010400u), cd1 = __builtin_amdgcn_perm(D, C, 0x07030602u);
-        const uint32_t r[4] = {__builtin_amdgcn_perm(cd0, ab0, 0x05040100u), __builtin_amdgcn_perm(cd0, ab0, 0x07060302u),
-                               __builtin_amdgcn_perm(cd1, ab1, 0x05040100u), __builtin_amdgcn_perm(cd1, ab1, 0x07060302u)};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (4 * h + q < P) out[4 * h + q][d] = r[q];
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < P; ++l)
-      store16<kBufNT>(sp[dst0 + l], off, make_uint4(out[l][0], out[l][1], out[l][2], out[l][3]), len);
+    ldsx_store<P>(acc, sp, dst0, off, len);
   }
 }
 
@@ -864,20 +878,30 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
 // ec_encode_glds, ms per launch: bench.py batch encode k20 p8 1.38 vs 1.57,
 // k16 p8 2.23 vs 2.46, k10 p8 3.08 vs 3.26, k10 p7 3.01 vs 3.05, same box
 // (profiles/r06/r06_wide_ldsx_bench_ab_b.jsonl). Below 7 rows it does not pay
-// in the library: k20 p6 1.30 vs 1.29 there (the standalone sweep,
-// r06_wide_ldsx_probe_b.jsonl, had it 5 % ahead on another layout), k10 p6
-// and k10 p4 within 1 %, k20 p4 3 % behind.
-constexpr int kLdsxRows = 5, kLdsxAutoRows = 7, kLdsxMaxK = 64;
+// in the library with loads in plain pairs: k20 p6 1.30 vs 1.29 there (the
+// standalone sweep, r06_wide_ldsx_probe_b.jsonl, had it 5 % ahead on another
+// layout), k10 p6 and k10 p4 within 1 %, k20 p4 3 % behind. With the pairs
+// double-buffered, two interleaved rounds on one box
+// (r06_wide_ldsx_pf_bench_ab.jsonl): 5-6 rows over k >= 16 sources gain
+// 0-2 % (k16 p6 1.97/1.98 vs 2.01/2.00 ms, k20 p6 1.27/1.29 vs 1.29/1.29,
+// k20 p5 1.25/1.25 vs 1.26/1.25), narrower stripes lose up to 2 % (k12 p5
+// 1.55 vs 1.52/1.54, k13 p6 1.74 vs 1.73) or are even (k10 p5, k10 p6).
+constexpr int kLdsxRows = 5, kLdsxAutoRows = 7, kLdsxWideK = 16, kLdsxMaxK = 64;
 bool enc_ldsx(int P, int k, const uint64_t* ldsx) {
   if (!ldsx || P < kLdsxRows || k > kLdsxMaxK) return false;
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_LDSX);
   if (v == 0 || v == 1) return v == 1;
-  return P >= kLdsxAutoRows;
+  return P >= kLdsxAutoRows || k >= kLdsxWideK;
 }
 
-// Sources loaded together by ec_encode_ldsx: 2 (the same sweep: 2-4 within 1 %
-// of each other, 1 and 5 up to 5 % slower — more loads in flight cost VGPRs,
-// and the lane already has 32 accumulator VGPRs live).
+// Sources per load group of ec_encode_ldsx: 2, double-buffered (the next
+// pair's loads issued before the current pair is folded). The standalone
+// sweep (r06_wide_ldsx_probe_c.jsonl, variant ldsx_pf2 against ldsx_u2 =
+// plain pairs): k20 p8 1.34/1.36 vs 1.37/1.38 ms, k16 p8 2.10/2.11 vs
+// 2.16/2.16, k20 p6 1.26/1.27 vs 1.32/1.31, k10 p7-p8 even. Plain groups of
+// 2-4 were within 1 % of each other, 1 and 5 up to 5 % slower, and sources
+// staged through a per-wave LDS-DMA ring (2-8 slots) 1-8 % slower than the
+// double-buffered pairs.
 constexpr int kLdsxGroup = 2;
 
 template <int P, int U>

@@ -93,6 +93,12 @@ __global__ __launch_bounds__(B) void skel_tiles(uint64_t data, uint64_t coding, 
 // use_ptrs: bit 0 the pointer table; bits 8-15 T, tiles per workgroup (1, 2
 // or 4; the xor_gen / pq_gen / C2 shapes only for T > 1); bits 16+ threads per
 // workgroup other than 256 (128, 512 or 1024; xor_gen and C2 only, T = 1).
+// Bytes between consecutive shards beyond len in the pointer table (0: the
+// shards abut, every one len-aligned like bench.py's (S, k, len) tensors):
+// whether the shards' alignment to each other changes the rate.
+static unsigned long long g_shard_pad = 0;
+extern "C" void skel_probe_set_pad(unsigned long long pad) { g_shard_pad = pad; }
+
 extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p, unsigned stripes, int reps,
                                  unsigned lds, int use_ptrs) {
   const int tpi = ((use_ptrs >> 8) & 255) ? ((use_ptrs >> 8) & 255) : 1;
@@ -135,9 +141,10 @@ extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p
     if (!h) return -5.0;
     for (unsigned st = 0; st < stripes; ++st) {
       for (int j = 0; j < k; ++j)
-        h[st * (k + p) + j] = reinterpret_cast<uint64_t>(data) + (static_cast<uint64_t>(st) * k + j) * len;
+        h[st * (k + p) + j] = reinterpret_cast<uint64_t>(data) + (static_cast<uint64_t>(st) * k + j) * (len + g_shard_pad);
       for (int l = 0; l < p; ++l)
-        h[st * (k + p) + k + l] = reinterpret_cast<uint64_t>(coding) + (static_cast<uint64_t>(st) * p + l) * len;
+        h[st * (k + p) + k + l] =
+            reinterpret_cast<uint64_t>(coding) + (static_cast<uint64_t>(st) * p + l) * (len + g_shard_pad);
     }
     const bool ok = hipMalloc(&d_ptrs, np * 8) == hipSuccess && hipMemcpy(d_ptrs, h, np * 8, hipMemcpyHostToDevice) == hipSuccess;
     free(h);

@@ -10,7 +10,8 @@ table as the batch encode does, instead of computed from the layout.
 `tiles_per_wg` (TILES=1,2,4 in the environment; the xor_gen / pq_gen / C2
 shapes only above 1): consecutive 4 KiB tiles per workgroup. `threads_per_wg`
 (BLOCKS=256,128,512,1024; xor_gen and C2 only besides 256): a tile is
-threads x 16 bytes.
+threads x 16 bytes. `shard_pad` (PAD=0,256,4096,... in the environment,
+pointer table only): bytes between consecutive shards beyond len.
 Run on the GPU box: python3 tools/skel_probe.py [REPS [SHAPE]]
 """
 import ctypes
@@ -55,11 +56,18 @@ def main():
         assert k * n * s <= data.numel() and p * n * s <= coding.numel()
         for blk in [int(b) for b in os.environ.get("BLOCKS", "256").split(",")]:
          for tpi in [int(t) for t in os.environ.get("TILES", "1").split(",")]:
-          for lds, ptrs in ((0, 0), (32768, 0), (32768, 1)):
+          pads = [int(x) for x in os.environ.get("PAD", "").split(",") if x]
+          combos = [(32768, 1, pad) for pad in pads] if pads else [(0, 0, 0), (32768, 0, 0), (32768, 1, 0)]
+          for lds, ptrs, pad in combos:
+            if pads:
+                if k * (n + pad) * s > data.numel() or p * (n + pad) * s > coding.numel():
+                    continue
+                lib.skel_probe_set_pad(ctypes.c_ulonglong(pad))
             code = ptrs | (tpi << 8) | ((blk if blk != 256 else 0) << 16)
             g = lib.skel_probe_gbs(data.data_ptr(), coding.data_ptr(), n, k, p, s, reps, lds, code)
             print(json.dumps({"shape": label, "k": k, "p": p, "len": n, "stripes": s, "lds_bytes": lds,
-                              "pointer_table": bool(ptrs), "tiles_per_wg": tpi, "threads_per_wg": blk,
+                              "pointer_table": bool(ptrs), "shard_pad": pad, "tiles_per_wg": tpi,
+                              "threads_per_wg": blk,
                               "reps": reps, "gb_s": round(g, 1), "frac_of_8tbs": round(g / 8000.0, 4)}),
                   flush=True)
 

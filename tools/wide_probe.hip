@@ -15,6 +15,12 @@
 // ds_read_b64, whatever P; the tables are conflict-free (32 entries x 8 B =
 // one bank row).
 //
+// The library ships this as ec_encode_ldsx (7-8 row passes). Variants here:
+//   glds        the library's encode with no product tables (ec_encode_glds)
+//   ldsx_uU     ec_encode_ldsx<P, U>: U sources loaded, then folded
+//   ldsx_pf2    pairs, the next pair's loads issued before the current is folded
+//   ldsx_ringR  sources staged through a per-wave LDS-DMA ring of R slots
+//
 //   usage: wide_probe [ITERS] [ROUNDS]   one JSON line per (shape, variant)
 //
 // Build: make -C isa-l_amd wide_probe (includes csrc/ec_kernels.hip).
@@ -30,106 +36,98 @@ extern "C" void isal_hip_kreg_add(const void*, const char*) {}
 
 namespace {
 
-struct L64 {
-  uint32_t lo, hi;
-};
-
-__device__ __forceinline__ uint32_t sdwa_add_b(uint32_t v, uint32_t base, int b) {
-  uint32_t r;
-  switch (b) {
-    case 0:
-      asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
-          : "=v"(r) : "v"(v), "v"(base));
-      break;
-    case 1:
-      asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
-          : "=v"(r) : "v"(v), "v"(base));
-      break;
-    case 2:
-      asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
-          : "=v"(r) : "v"(v), "v"(base));
-      break;
-    default:
-      asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
-          : "=v"(r) : "v"(v), "v"(base));
-      break;
-  }
-  return r;
-}
-
-__device__ __forceinline__ uint64_t lds64(uint32_t addr) {
-  return *reinterpret_cast<const __attribute__((address_space(3))) uint64_t*>(static_cast<uintptr_t>(addr));
-}
-
-// acc[4d + b] ^= T5_j[field5(byte b of dword d)] ^ T3_j[field3(...)] for one 16-byte source chunk
-__device__ __forceinline__ void ldsx_acc(L64 (&acc)[16], const uint4& x, uint32_t b5, uint32_t b3) {
-  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t lo8 = (w[d] << 3) & 0xF8F8F8F8u;  // bits 0-4 of each byte, times 8
-    const uint32_t hi8 = (w[d] >> 2) & 0x38383838u;  // bits 5-7 of each byte, times 8
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const uint64_t p = lds64(sdwa_add_b(lo8, b5, b));
-      const uint64_t q = lds64(sdwa_add_b(hi8, b3, b));
-      L64& a = acc[4 * d + b];
-      a.lo = xor3(a.lo, static_cast<uint32_t>(p), static_cast<uint32_t>(q));
-      a.hi = xor3(a.hi, static_cast<uint32_t>(p >> 32), static_cast<uint32_t>(q >> 32));
-    }
-  }
-}
-
-template <int P, int U>
-__global__ __launch_bounds__(kBlock) void enc_ldsx(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
-                                                   int dst0, const uint64_t* __restrict__ ltg, int len, int k,
-                                                   unsigned nitems, unsigned tiles) {
-  extern __shared__ uint64_t lt[];  // [k][32] T5, then [k][8] T3
-  for (int i = threadIdx.x; i < k * 40; i += kBlock) lt[i] = ltg[i];
+// ec_encode_ldsx with the next pair's loads issued before the current pair is
+// folded (register double buffer: 4 loads in flight per wave instead of 2)
+template <int P>
+__global__ __launch_bounds__(kBlock) void ldsx_pf(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
+                                                  int dst0, const uint64_t* __restrict__ ltg, int len, int k,
+                                                  unsigned nitems, unsigned tiles) {
+  extern __shared__ uint64_t lt[];
+  for (int i = threadIdx.x; i < k * ISAL_HIP_LDSX_ENTRIES; i += kBlock) lt[i] = ltg[i];
   __syncthreads();
-  const uint32_t lbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint64_t*)lt));
+  const uint32_t base5 = lds_off(lt), base3 = base5 + static_cast<uint32_t>(k) * 256u;
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     const unsigned v = xcd_item(w, nitems, 1);
     const unsigned stripe = v / tiles, tile = v - stripe * tiles;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
     const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
     if (off + kVec > len) continue;  // the probe's shapes have len % 4096 == 0
-    L64 acc[16];
+    Acc64 acc[16];
 #pragma unroll
-    for (int p = 0; p < 16; ++p) acc[p] = L64{0u, 0u};
-    int j = 0;
-    for (; j + U <= k; j += U) {
-      uint4 x[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) x[u] = load16<kBufNT>(sp[src0 + j + u], off, len);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        ldsx_acc(acc, x[u], lbase + (j + u) * 256u, lbase + k * 256u + (j + u) * 64u);
+    for (int q = 0; q < 16; ++q) acc[q] = Acc64{0u, 0u};
+    uint4 a0 = load16<kBufNT>(sp[src0], off, len);
+    uint4 a1 = k > 1 ? load16<kBufNT>(sp[src0 + 1], off, len) : make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < k; j += 2) {
+      uint4 b0 = make_uint4(0, 0, 0, 0), b1 = make_uint4(0, 0, 0, 0);
+      if (j + 2 < k) b0 = load16<kBufNT>(sp[src0 + j + 2], off, len);
+      if (j + 3 < k) b1 = load16<kBufNT>(sp[src0 + j + 3], off, len);
+      ldsx_acc(acc, a0, base5 + j * 256u, base3 + j * 64u);
+      if (j + 1 < k) ldsx_acc(acc, a1, base5 + (j + 1) * 256u, base3 + (j + 1) * 64u);
+      a0 = b0;
+      a1 = b1;
     }
-    for (; j < k; ++j) {
-      const uint4 x = load16<kBufNT>(sp[src0 + j], off, len);
-      ldsx_acc(acc, x, lbase + j * 256u, lbase + k * 256u + j * 64u);
+    ldsx_store<P>(acc, sp, dst0, off, len);
+  }
+}
+
+// ec_encode_ldsx with the sources staged through a per-wave LDS-DMA ring of R
+// 1-KiB slots, as ec_encode_glds: R loads in flight all the time, no VGPRs
+template <int P, int R>
+__global__ __launch_bounds__(kBlock) void ldsx_ring(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
+                                                    int dst0, const uint64_t* __restrict__ ltg, int len, int k,
+                                                    unsigned nitems, unsigned tiles) {
+  static_assert(R % 2 == 0 && R >= 2 && R <= 8, "ring of 2..8 slots, folded in pairs");
+  extern __shared__ uint64_t lt[];
+  const int ltn = k * ISAL_HIP_LDSX_ENTRIES;
+  for (int i = threadIdx.x; i < ltn; i += kBlock) lt[i] = ltg[i];
+  __syncthreads();
+  const uint32_t base5 = lds_off(lt), base3 = base5 + static_cast<uint32_t>(k) * 256u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ring = base5 + ((static_cast<uint32_t>(ltn) * 8 + 1023) & ~1023u) + wave * (R * 1024);
+  const uint32_t mine = ring + (threadIdx.x & 63) * kVec;
+  for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
+    const unsigned v = xcd_item(w, nitems, 1);
+    const unsigned stripe = v / tiles, tile = v - stripe * tiles;
+    const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
+    const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
+    if (static_cast<long long>(tile + 1) * kTile > len) continue;  // full tiles only in the probe
+    vm_wait<0>();
+    const uint32_t voff = static_cast<uint32_t>(off);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (r < k) glds16(sp[src0 + r], voff, ring + r * 1024);
+    Acc64 acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = Acc64{0u, 0u};
+    for (int j0 = 0; j0 < k; j0 += R) {
+      auto step = [&](auto rc) {
+        constexpr int r = decltype(rc)::value * 2;
+        const int j = j0 + r;
+        if (j >= k) return;
+        uint4 x0, x1;
+        if (j + 1 < k) {
+          if (j + R <= k)
+            vm_wait<R - 2>();
+          else
+            vm_wait_rt(k - 2 - j);
+          lds_read2<r * 1024, (r + 1) * 1024>(x0, x1, mine);
+          if (j + R < k) glds16(sp[src0 + j + R], voff, ring + r * 1024);
+          if (j + 1 + R < k) glds16(sp[src0 + j + 1 + R], voff, ring + (r + 1) * 1024);
+          __builtin_amdgcn_sched_barrier(0);
+          ldsx_acc(acc, x0, base5 + j * 256u, base3 + j * 64u);
+          ldsx_acc(acc, x1, base5 + (j + 1) * 256u, base3 + (j + 1) * 64u);
+        } else {
+          vm_wait<0>();
+          lds_read1<r * 1024>(x0, mine);
+          __builtin_amdgcn_sched_barrier(0);
+          ldsx_acc(acc, x0, base5 + j * 256u, base3 + j * 64u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      static_for(step, std::make_integer_sequence<int, R / 2>{});
     }
-    // transpose: row l, dword d = byte l of acc[4d..4d+3] (rows 0-3 in .lo, 4-7 in .hi)
-    uint32_t out[P][4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && P <= 4) continue;
-        const uint32_t A = h ? acc[4 * d].hi : acc[4 * d].lo, B = h ? acc[4 * d + 1].hi : acc[4 * d + 1].lo;
-        const uint32_t C = h ? acc[4 * d + 2].hi : acc[4 * d + 2].lo, D = h ? acc[4 * d + 3].hi : acc[4 * d + 3].lo;
-        const uint32_t ab0 = __builtin_amdgcn_perm(B, A, 0x05010400u), ab1 = __builtin_amdgcn_perm(B, A, 0x07030602u);
-        const uint32_t cd0 = __builtin_amdgcn_perm(D, C, 0x05010400u), cd1 = __builtin_amdgcn_perm(D, C, 0x07030602u);
-        const uint32_t r[4] = {__builtin_amdgcn_perm(cd0, ab0, 0x05040100u), __builtin_amdgcn_perm(cd0, ab0, 0x07060302u),
-                               __builtin_amdgcn_perm(cd1, ab1, 0x05040100u), __builtin_amdgcn_perm(cd1, ab1, 0x07060302u)};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (4 * h + q < P) out[4 * h + q][d] = r[q];
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < P; ++l)
-      store16<kBufNT>(sp[dst0 + l], off, make_uint4(out[l][0], out[l][1], out[l][2], out[l][3]), len);
+    vm_wait<0>();
+    ldsx_store<P>(acc, sp, dst0, off, len);
   }
 }
 
@@ -158,33 +156,54 @@ struct Shape {
   int k, p, len, ns;
 };
 
-template <int P, int U>
-static void launch_ldsx(unsigned grid, const uint64_t* dp, int stride, const uint64_t* dlt, int len, int k,
-                        unsigned nitems, unsigned tiles) {
-  hipLaunchKernelGGL((enc_ldsx<P, U>), dim3(grid), dim3(kBlock), static_cast<size_t>(k) * 40 * 8, 0, dp, stride, 0, k,
-                     dlt, len, k, nitems, tiles);
+// V: 1..5 the library's ec_encode_ldsx<P, V>; 10 + R the LDS-DMA ring of R slots; 20 the prefetch
+template <int P>
+static void launch_var(int V, unsigned grid, const uint64_t* dp, int stride, const uint32_t* dt, const uint64_t* dlt,
+                       int len, int k, unsigned nitems, unsigned tiles) {
+  const size_t lt = static_cast<size_t>(k) * ISAL_HIP_LDSX_ENTRIES * 8, ringb = (lt + 1023) & ~size_t(1023);
+  switch (V) {
+#define LIB(u)                                                                                                   \
+  case u:                                                                                                        \
+    hipLaunchKernelGGL((ec_encode_ldsx<P, u>), dim3(grid), dim3(kBlock), lt, 0, dp, stride, 0, k, dt, dlt, len, k, \
+                       nitems, tiles);                                                                           \
+    return;
+    LIB(1) LIB(2) LIB(3) LIB(4)
+#undef LIB
+#define RING(r)                                                                                                  \
+  case 10 + r:                                                                                                   \
+    hipLaunchKernelGGL((ldsx_ring<P, r>), dim3(grid), dim3(kBlock), ringb + 4 * r * 1024, 0, dp, stride, 0, k, dlt, \
+                       len, k, nitems, tiles);                                                                   \
+    return;
+    RING(2) RING(4) RING(6) RING(8)
+#undef RING
+    case 20:
+      hipLaunchKernelGGL((ldsx_pf<P>), dim3(grid), dim3(kBlock), lt, 0, dp, stride, 0, k, dlt, len, k, nitems, tiles);
+      return;
+  }
+  fprintf(stderr, "no variant %d\n", V);
+  exit(1);
 }
 
-static void ldsx(int P, int U, unsigned grid, const uint64_t* dp, int stride, const uint64_t* dlt, int len, int k,
-                 unsigned nitems, unsigned tiles) {
-#define L(p, u) \
-  if (P == p && U == u) return launch_ldsx<p, u>(grid, dp, stride, dlt, len, k, nitems, tiles);
-#define LU(p) L(p, 1) L(p, 2) L(p, 3) L(p, 4) L(p, 5)
-  LU(3) LU(4) LU(5) LU(6) LU(7) LU(8)
-#undef LU
-#undef L
-  fprintf(stderr, "no instantiation P=%d U=%d\n", P, U);
+static void ldsx(int P, int V, unsigned grid, const uint64_t* dp, int stride, const uint32_t* dt, const uint64_t* dlt,
+                 int len, int k, unsigned nitems, unsigned tiles) {
+  switch (P) {
+    case 4: return launch_var<4>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
+    case 5: return launch_var<5>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
+    case 6: return launch_var<6>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
+    case 7: return launch_var<7>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
+    case 8: return launch_var<8>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
+  }
+  fprintf(stderr, "no instantiation P=%d\n", P);
   exit(1);
 }
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 10;
   const int rounds = argc > 2 ? atoi(argv[2]) : 2;
-  const Shape shapes[] = {{10, 4, 1 << 20, 1024}, {10, 3, 1 << 20, 1024}, {10, 5, 1 << 20, 1024},
-                          {10, 6, 1 << 20, 1024}, {10, 7, 1 << 20, 1024}, {10, 8, 1 << 20, 1024},
-                          {20, 4, 4 << 20, 64},    {20, 5, 4 << 20, 64},    {20, 6, 4 << 20, 64},
-                          {20, 7, 4 << 20, 64},    {20, 8, 4 << 20, 64},    {8, 6, 1 << 20, 1024},
-                          {16, 8, 1 << 20, 512},   {12, 4, 1 << 20, 1024}};
+  const Shape shapes[] = {{10, 4, 1 << 20, 1024}, {10, 5, 1 << 20, 1024}, {10, 6, 1 << 20, 1024},
+                          {10, 7, 1 << 20, 1024}, {10, 8, 1 << 20, 1024}, {16, 8, 1 << 20, 512},
+                          {20, 5, 4 << 20, 64},    {20, 6, 4 << 20, 64},    {20, 8, 4 << 20, 64},
+                          {13, 6, 1 << 20, 512}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -211,15 +230,8 @@ int main(int argc, char** argv) {
       uint32_t* dt = nullptr;
       CK(hipMalloc(&dt, ht.size() * 4));
       CK(hipMemcpy(dt, ht.data(), ht.size() * 4, hipMemcpyHostToDevice));
-      std::vector<uint64_t> hl(static_cast<size_t>(k) * 40, 0);
-      for (int j = 0; j < k; ++j)
-        for (int l = 0; l < p; ++l) {
-          const unsigned char c = a[(k + l) * k + j];
-          for (int v = 0; v < 32; ++v)
-            hl[j * 32 + v] |= static_cast<uint64_t>(gf_mul(c, static_cast<unsigned char>(v))) << (8 * l);
-          for (int v = 0; v < 8; ++v)
-            hl[k * 32 + j * 8 + v] |= static_cast<uint64_t>(gf_mul(c, static_cast<unsigned char>(v << 5))) << (8 * l);
-        }
+      std::vector<uint64_t> hl(isal_hip_ldsx_words(k, p));
+      isal_hip_build_ldsx_tables(k, p, g.data(), hl.data());
       uint64_t* dl = nullptr;
       CK(hipMalloc(&dl, hl.size() * 8));
       CK(hipMemcpy(dl, hl.data(), hl.size() * 8, hipMemcpyHostToDevice));
@@ -237,14 +249,15 @@ int main(int argc, char** argv) {
         int U;
         unsigned grid;
       };
-      const Var vars[] = {{"lib", 0, 0},         {"ldsx_u1", 1, nitems}, {"ldsx_u2", 2, nitems},
-                          {"ldsx_u3", 3, nitems}, {"ldsx_u4", 4, nitems}, {"ldsx_u5", 5, nitems}};
+      const Var vars[] = {{"glds", 0, 0},       {"ldsx_u2", 2, nitems},   {"ldsx_u4", 4, nitems},
+                          {"ldsx_pf2", 20, nitems}, {"ldsx_ring2", 12, nitems}, {"ldsx_ring4", 14, nitems},
+                          {"ldsx_ring6", 16, nitems}, {"ldsx_ring8", 18, nitems}};
       for (const Var& var : vars) {
         auto go = [&]() {
           if (!var.U)
             CK(static_cast<hipError_t>(isal_hip_launch_encode(dp, stride, 0, k, dt, len, k, p, ns, 1, &em, nullptr)));
           else
-            ldsx(p, var.U, var.grid < nitems ? var.grid : nitems, dp, stride, dl, len, k, nitems, tiles);
+            ldsx(p, var.U, var.grid < nitems ? var.grid : nitems, dp, stride, dt, dl, len, k, nitems, tiles);
         };
         CK(hipMemset(d + (probe_stripe * stride + k) * shard, 0xA5, shard * p));
         go();
