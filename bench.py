@@ -251,14 +251,14 @@ def enc_kernel(rows: int, k: int, coef) -> str:
     of 5-8 rows stage their sources through the LDS-DMA ring (ec_encode_glds,
     4 slots per wave, table halves from LDS; ISAL_HIP_ENC_GLDS=0 off) unless
     they look their products up in LDS product tables (ec_encode_ldsx: 7-8
-    rows, or 5-6 rows over k >= 16, k <= 64; ISAL_HIP_ENC_LDSX=1 every 5-8
+    rows, or 5-6 rows over k >= 16, k <= 64; ISAL_HIP_ENC_LDSX=1 every 4-8
     row pass, =0 off). The library names the same instantiation on stderr with
     ISAL_HIP_LOG=2."""
     import numpy as np
 
     c = np.asarray(coef, dtype=np.uint8).reshape(rows, k)
     ldsx = os.environ.get("ISAL_HIP_ENC_LDSX")
-    if rows >= 5 and k <= 64 and ldsx != "0" and (ldsx == "1" or rows >= 7 or k >= 16):
+    if rows >= 4 and k <= 64 and ldsx != "0" and (ldsx == "1" or rows >= 7 or (rows >= 5 and k >= 16)):
         # LDS product tables (ec_kernels.hip enc_ldsx, kLdsxGroup); batches and pipelines upload them
         return f"ec_encode_ldsx<{rows}, 2>"
     fl = 0

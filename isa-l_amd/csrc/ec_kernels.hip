@@ -874,7 +874,7 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
 
 // Passes of 7-8 rows over at most kLdsxMaxK sources take the LDS product
 // tables (ec_encode_ldsx) when the caller uploaded them (isal_hip_encmask.ldsx;
-// ISAL_HIP_ENC_LDSX=1: every pass of 5-8 rows, =0 off). Against
+// ISAL_HIP_ENC_LDSX=1: every pass of 4-8 rows, =0 off). Against
 // ec_encode_glds, ms per launch: bench.py batch encode k20 p8 1.38 vs 1.57,
 // k16 p8 2.23 vs 2.46, k10 p8 3.08 vs 3.26, k10 p7 3.01 vs 3.05, same box
 // (profiles/r06/r06_wide_ldsx_bench_ab_b.jsonl). Below 7 rows it does not pay
@@ -886,12 +886,12 @@ void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stri
 // 0-2 % (k16 p6 1.97/1.98 vs 2.01/2.00 ms, k20 p6 1.27/1.29 vs 1.29/1.29,
 // k20 p5 1.25/1.25 vs 1.26/1.25), narrower stripes lose up to 2 % (k12 p5
 // 1.55 vs 1.52/1.54, k13 p6 1.74 vs 1.73) or are even (k10 p5, k10 p6).
-constexpr int kLdsxRows = 5, kLdsxAutoRows = 7, kLdsxWideK = 16, kLdsxMaxK = 64;
+constexpr int kLdsxRows = 4, kLdsxAutoRows = 7, kLdsxWideRows = 5, kLdsxWideK = 16, kLdsxMaxK = 64;
 bool enc_ldsx(int P, int k, const uint64_t* ldsx) {
   if (!ldsx || P < kLdsxRows || k > kLdsxMaxK) return false;
   const long long v = isal_hip_knob(ISAL_HIP_KNOB_ENC_LDSX);
   if (v == 0 || v == 1) return v == 1;
-  return P >= kLdsxAutoRows || k >= kLdsxWideK;
+  return P >= kLdsxAutoRows || (P >= kLdsxWideRows && k >= kLdsxWideK);
 }
 
 // Sources per load group of ec_encode_ldsx: 2, double-buffered (the next

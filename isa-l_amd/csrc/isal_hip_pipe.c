@@ -114,7 +114,7 @@ isal_hip_pipe_create(isal_hip_pipe **out, int len, int k, int rows, const unsign
                     hipMemcpy(p->d_tbl, h_tbl, ntbl * 4, hipMemcpyHostToDevice) != hipSuccess)
                         rc = ISAL_HIP_EHIP;
         }
-        if (rc == ISAL_HIP_OK && mode == ISAL_HIP_PIPE_ENCODE && k <= 64 && rows >= 5) {
+        if (rc == ISAL_HIP_OK && mode == ISAL_HIP_PIPE_ENCODE && k <= 64 && rows >= 4) {
                 /* the wide passes' LDS product tables (ec_encode_ldsx) */
                 const size_t nw = isal_hip_ldsx_words(k, rows);
                 uint64_t *hx = (uint64_t *) malloc(nw * 8);

@@ -2196,8 +2196,8 @@ batch_set_tables_impl(isal_hip_batch *b, const unsigned char *gftbls)
                 e = hipMemcpy(b->d_tbl, h, n * 4, hipMemcpyHostToDevice);
         free(h);
         /* the wide passes' LDS product tables (ec_encode_ldsx): k <= 64, a
-         * pass of at least 5 rows */
-        if (e == hipSuccess && b->k >= 1 && b->k <= 64 && b->rows >= 5) {
+         * pass of at least 4 rows (4 only when ISAL_HIP_ENC_LDSX=1 forces it) */
+        if (e == hipSuccess && b->k >= 1 && b->k <= 64 && b->rows >= 4) {
                 const size_t nw = isal_hip_ldsx_words(b->k, b->rows);
                 uint64_t *hx = (uint64_t *) malloc(nw * 8);
                 if (!hx)

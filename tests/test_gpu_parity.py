@@ -1845,6 +1845,7 @@ def test_bench_rccl_control_plane_single_rank(gpu):
     (["--k", "20", "--p", "6", "--len", "262144", "--stripes", "8"], {}),  # 6 rows over k >= 16: product tables
     (["--k", "13", "--p", "6", "--len", "262144", "--stripes", "8"], {}),  # 6 rows over k < 16: the LDS-DMA ring
     (["--k", "7", "--p", "5"], {"ISAL_HIP_ENC_LDSX": "1"}),           # product tables forced, odd k
+    (["--k", "10", "--p", "4"], {"ISAL_HIP_ENC_LDSX": "1"}),          # product tables forced on 4 rows
     (["--k", "10", "--p", "8"], {"ISAL_HIP_ENC_LDSX": "0"}),          # 8 rows: the LDS-DMA ring
     (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_WIDE5": "0", "ISAL_HIP_ENC_GLDS": "0", "ISAL_HIP_ENC_LDSX": "0"}),
     (["--k", "10", "--p", "6"], {"ISAL_HIP_ENC_LDS": "0", "ISAL_HIP_ENC_XOR": "0", "ISAL_HIP_ENC_GLDS": "0",

@@ -21,7 +21,12 @@
 //   ldsx_pf2    pairs, the next pair's loads issued before the current is folded
 //   ldsx_ringR  sources staged through a per-wave LDS-DMA ring of R slots
 //
-//   usage: wide_probe [ITERS] [ROUNDS]   one JSON line per (shape, variant)
+// Round-6 final form: the library's ec_encode_ldsx<P, 2> (double-buffered
+// pairs) at several occupancy caps (dynamic LDS per workgroup) beside the
+// library's encode, in bench.py's shard layout (LAYOUT 1) or with each
+// stripe's shards back to back (0, the layout of the sweeps above).
+//
+//   usage: wide_probe [ITERS] [ROUNDS] [LAYOUT]   one JSON line per (shape, variant)
 //
 // Build: make -C isa-l_amd wide_probe (includes csrc/ec_kernels.hip).
 #include "../isa-l_amd/csrc/ec_kernels.hip"
@@ -159,8 +164,9 @@ struct Shape {
 // V: 1..5 the library's ec_encode_ldsx<P, V>; 10 + R the LDS-DMA ring of R slots; 20 the prefetch
 template <int P>
 static void launch_var(int V, unsigned grid, const uint64_t* dp, int stride, const uint32_t* dt, const uint64_t* dlt,
-                       int len, int k, unsigned nitems, unsigned tiles) {
-  const size_t lt = static_cast<size_t>(k) * ISAL_HIP_LDSX_ENTRIES * 8, ringb = (lt + 1023) & ~size_t(1023);
+                       int len, int k, unsigned nitems, unsigned tiles, size_t cap) {
+  const size_t lt0 = static_cast<size_t>(k) * ISAL_HIP_LDSX_ENTRIES * 8, ringb = (lt0 + 1023) & ~size_t(1023);
+  const size_t lt = lt0 > cap ? lt0 : cap;  // dynamic LDS as an occupancy cap
   switch (V) {
 #define LIB(u)                                                                                                   \
   case u:                                                                                                        \
@@ -185,13 +191,13 @@ static void launch_var(int V, unsigned grid, const uint64_t* dp, int stride, con
 }
 
 static void ldsx(int P, int V, unsigned grid, const uint64_t* dp, int stride, const uint32_t* dt, const uint64_t* dlt,
-                 int len, int k, unsigned nitems, unsigned tiles) {
+                 int len, int k, unsigned nitems, unsigned tiles, size_t cap) {
   switch (P) {
-    case 4: return launch_var<4>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
-    case 5: return launch_var<5>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
-    case 6: return launch_var<6>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
-    case 7: return launch_var<7>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
-    case 8: return launch_var<8>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles);
+    case 4: return launch_var<4>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles, cap);
+    case 5: return launch_var<5>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles, cap);
+    case 6: return launch_var<6>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles, cap);
+    case 7: return launch_var<7>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles, cap);
+    case 8: return launch_var<8>(V, grid, dp, stride, dt, dlt, len, k, nitems, tiles, cap);
   }
   fprintf(stderr, "no instantiation P=%d\n", P);
   exit(1);
@@ -200,10 +206,13 @@ static void ldsx(int P, int V, unsigned grid, const uint64_t* dp, int stride, co
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 10;
   const int rounds = argc > 2 ? atoi(argv[2]) : 2;
-  const Shape shapes[] = {{10, 4, 1 << 20, 1024}, {10, 5, 1 << 20, 1024}, {10, 6, 1 << 20, 1024},
-                          {10, 7, 1 << 20, 1024}, {10, 8, 1 << 20, 1024}, {16, 8, 1 << 20, 512},
-                          {20, 5, 4 << 20, 64},    {20, 6, 4 << 20, 64},    {20, 8, 4 << 20, 64},
-                          {13, 6, 1 << 20, 512}};
+  // layout 1 (default): bench.py's — the sources of all stripes in one buffer
+  // (stripe s, source j at (s k + j) len), the parity rows in another; layout
+  // 0: each stripe's k + p shards back to back in one buffer
+  const int layout = argc > 3 ? atoi(argv[3]) : 1;
+  const Shape shapes[] = {{10, 4, 1 << 20, 1024}, {12, 4, 1 << 20, 1024}, {10, 6, 1 << 20, 1024},
+                          {10, 8, 1 << 20, 1024}, {16, 8, 1 << 20, 512},  {13, 6, 1 << 20, 512},
+                          {20, 6, 4 << 20, 64},   {20, 8, 4 << 20, 64}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -211,12 +220,18 @@ int main(int argc, char** argv) {
     for (const Shape& s : shapes) {
       const int k = s.k, p = s.p, len = s.len, ns = s.ns, stride = k + p;
       const size_t shard = static_cast<size_t>(len);
-      uint8_t* d = nullptr;
-      CK(hipMalloc(&d, shard * stride * ns));
-      hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t*>(d), shard * stride * ns / 8,
-                         777ull + k * 31 + p);
+      uint8_t *d = nullptr, *c = nullptr;
+      CK(hipMalloc(&d, shard * (layout ? k : stride) * ns));
+      if (layout) CK(hipMalloc(&c, shard * p * ns));
+      hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t*>(d),
+                         shard * (layout ? k : stride) * ns / 8, 777ull + k * 31 + p);
       std::vector<uint64_t> hp(static_cast<size_t>(stride) * ns);
-      for (size_t i = 0; i < hp.size(); ++i) hp[i] = reinterpret_cast<uint64_t>(d + i * shard);
+      auto at = [&](size_t st, int i) -> uint8_t* {
+        if (!layout) return d + (st * stride + i) * shard;
+        return i < k ? d + (st * k + i) * shard : c + (st * p + (i - k)) * shard;
+      };
+      for (int st = 0; st < ns; ++st)
+        for (int i = 0; i < stride; ++i) hp[static_cast<size_t>(st) * stride + i] = reinterpret_cast<uint64_t>(at(st, i));
       uint64_t* dp = nullptr;
       CK(hipMalloc(&dp, hp.size() * 8));
       CK(hipMemcpy(dp, hp.data(), hp.size() * 8, hipMemcpyHostToDevice));
@@ -237,34 +252,33 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(dl, hl.data(), hl.size() * 8, hipMemcpyHostToDevice));
       const unsigned tiles = len / kTile, nitems = tiles * ns;
       const double bytes = static_cast<double>(stride) * shard * ns;
-      // reference parity: the library's encode
+      // reference parity: the library's encode without product tables
       std::vector<uint8_t> ref(shard * p), got(shard * p);
       CK(static_cast<hipError_t>(isal_hip_launch_encode(dp, stride, 0, k, dt, len, k, p, ns, 1, &em, nullptr)));
       CK(hipDeviceSynchronize());
       const size_t probe_stripe = ns - 1;
-      for (int l = 0; l < p; ++l)
-        CK(hipMemcpy(ref.data() + l * shard, d + (probe_stripe * stride + k + l) * shard, shard, hipMemcpyDeviceToHost));
+      for (int l = 0; l < p; ++l) CK(hipMemcpy(ref.data() + l * shard, at(probe_stripe, k + l), shard, hipMemcpyDeviceToHost));
       struct Var {
         const char* name;
         int U;
-        unsigned grid;
+        size_t cap;
       };
-      const Var vars[] = {{"glds", 0, 0},       {"ldsx_u2", 2, nitems},   {"ldsx_u4", 4, nitems},
-                          {"ldsx_pf2", 20, nitems}, {"ldsx_ring2", 12, nitems}, {"ldsx_ring4", 14, nitems},
-                          {"ldsx_ring6", 16, nitems}, {"ldsx_ring8", 18, nitems}};
+      // lib: the library's encode without product tables (v16 / glds); ldsx_capN:
+      // ec_encode_ldsx<P, 2> with N KiB of dynamic LDS (0: its tables only)
+      const Var vars[] = {{"lib", 0, 0},           {"ldsx_cap0", 2, 0},       {"ldsx_cap20", 2, 20 << 10},
+                          {"ldsx_cap24", 2, 24 << 10}, {"ldsx_cap32", 2, 32 << 10}, {"ldsx_cap40", 2, 40 << 10}};
       for (const Var& var : vars) {
         auto go = [&]() {
           if (!var.U)
             CK(static_cast<hipError_t>(isal_hip_launch_encode(dp, stride, 0, k, dt, len, k, p, ns, 1, &em, nullptr)));
           else
-            ldsx(p, var.U, var.grid < nitems ? var.grid : nitems, dp, stride, dt, dl, len, k, nitems, tiles);
+            ldsx(p, var.U, nitems, dp, stride, dt, dl, len, k, nitems, tiles, var.cap);
         };
-        CK(hipMemset(d + (probe_stripe * stride + k) * shard, 0xA5, shard * p));
+        for (int l = 0; l < p; ++l) CK(hipMemset(at(probe_stripe, k + l), 0xA5, shard));
         go();
         CK(hipDeviceSynchronize());
         CK(hipGetLastError());
-        for (int l = 0; l < p; ++l)
-          CK(hipMemcpy(got.data() + l * shard, d + (probe_stripe * stride + k + l) * shard, shard, hipMemcpyDeviceToHost));
+        for (int l = 0; l < p; ++l) CK(hipMemcpy(got.data() + l * shard, at(probe_stripe, k + l), shard, hipMemcpyDeviceToHost));
         const bool ok = memcmp(ref.data(), got.data(), shard * p) == 0;
         for (int w = 0; w < 2; ++w) go();
         CK(hipEventRecord(e0, 0));
@@ -274,12 +288,13 @@ int main(int argc, char** argv) {
         float ms = 0;
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= iters;
-        printf("{\"round\": %d, \"k\": %d, \"p\": %d, \"len\": %d, \"stripes\": %d, \"variant\": \"%s\", \"ms\": %.4f, "
-               "\"frac\": %.4f, \"bit_exact\": %s}\n",
-               round, k, p, len, ns, var.name, ms, bytes / ms / 1e6 / 8000.0, ok ? "true" : "false");
+        printf("{\"round\": %d, \"layout\": %d, \"k\": %d, \"p\": %d, \"len\": %d, \"stripes\": %d, \"variant\": \"%s\", "
+               "\"ms\": %.4f, \"frac\": %.4f, \"bit_exact\": %s}\n",
+               round, layout, k, p, len, ns, var.name, ms, bytes / ms / 1e6 / 8000.0, ok ? "true" : "false");
         fflush(stdout);
       }
       CK(hipFree(d));
+      if (c) CK(hipFree(c));
       CK(hipFree(dp));
       CK(hipFree(dt));
       CK(hipFree(dl));
