@@ -253,62 +253,79 @@ __global__ __launch_bounds__(kBlock) void crc64_shards_pre(const uint64_t* __res
   }
 }
 
-// v(L) <- sum over lanes of Z^(16 * (255 - L)) v(L), result in red[0]:
-// 8 levels, level s joins lanes L and L + 2^s with Z^(16 * 2^s).
-__device__ __forceinline__ uint64_t lane_tree(uint64_t* red, const uint64_t* tree) {
-  for (int s = 0; s < 8; ++s) {
-    const int step = 1 << s;
-    if ((threadIdx.x & (2 * step - 1)) == 0)
-      red[threadIdx.x] = apply_op(tree + s * kOp, red[threadIdx.x]) ^ red[threadIdx.x + step];
-    __syncthreads();
+// Sum over L < 256 of Z^(16 * (255 - L)) v(L), lane l of a wave holding
+// v(4l .. 4l + 3): a Horner step with Z^16 inside the lane, then six shuffle
+// levels, level s joining lanes l and l + 2^s with Z^(64 * 2^s) (OP_TREE
+// s + 2). The result is in lane 0 (lanes the result does not depend on read
+// past the wave and compute garbage). No barriers: one wave per shard.
+static_assert(kBlock == 256, "wave_fold: 4 lane positions per lane of a 64-lane wave");
+__device__ __forceinline__ uint64_t wave_fold(const uint64_t* tree, const uint64_t (&v)[4]) {
+  uint64_t h = v[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) h = apply_op(tree, h) ^ v[i];
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const uint32_t lo = __shfl_down(static_cast<uint32_t>(h), 1u << s, 64);
+    const uint32_t hi = __shfl_down(static_cast<uint32_t>(h >> 32), 1u << s, 64);
+    h = apply_op(tree + (s + 2) * kOp, h) ^ ((static_cast<uint64_t>(hi) << 32) | lo);
   }
-  const uint64_t r = red[0];
-  __syncthreads();
-  return r;
+  return h;
 }
 
-// One workgroup per shard (grid-stride):
-//  X = raw(0, full tiles): each lane folds its block chains (Horner with
-//      Z^(4096*tt), the last block Z^(4096*nfull_last)), then the lane tree;
-//  T = raw(0, the tail's whole 16-byte chunks): lane chunks right-aligned in
-//      the tree, so lane q-1's chunk is the last one;
+// One wave per shard (grid-stride, four shards per workgroup at a time, the
+// tables loaded once per workgroup):
+//  X = raw(0, full tiles): lane l folds the block chains of lanes 4l..4l+3
+//      (Horner with Z^(4096*tt), the last block Z^(4096*nfull_last)), then
+//      wave_fold;
+//  T = raw(0, the tail's whole 16-byte chunks): chunks right-aligned over the
+//      256 lane positions, so the last chunk sits at position 255;
 //  s = Z^(16q)(X) ^ T, then the last tail % 16 bytes one at a time;
 //  crc64 = ~(Z^len(~init) ^ s).
+// (Round 5 ran one 256-lane workgroup per shard with an 8-level LDS tree and
+// a barrier per level: 0.13 ms per C2 batch, 5 % of the checksum pass.)
 template <bool REFL>
 __global__ __launch_bounds__(kBlock) void crc64_combine(
     const uint64_t* __restrict__ part, const uint64_t* __restrict__ ptrs, int ptr_stride, int nsh,
     int len, unsigned nblk, unsigned nfull, const uint64_t* __restrict__ tabs, uint64_t init_term,
     uint64_t* __restrict__ out, unsigned nshard_total) {
+  constexpr unsigned kWaves = kBlock / 64;
   __shared__ uint64_t lt[ISAL_HIP_CRC64_COMBINE_ENTRIES];
-  __shared__ uint64_t red[kBlock];
   load_lds<ISAL_HIP_CRC64_COMBINE_ENTRIES>(lt, tabs);
   __syncthreads();
   const int tail = len - static_cast<int>(nfull) * kTile;
   const int q = tail / kVec, rem = tail - q * kVec;
-  for (unsigned sh = blockIdx.x; sh < nshard_total; sh += gridDim.x) {
+  const unsigned lane = threadIdx.x & 63;
+  const uint64_t* tree = lt + ISAL_HIP_CRC64_OP_TREE;
+  for (unsigned sh = blockIdx.x * kWaves + (threadIdx.x >> 6); sh < nshard_total; sh += gridDim.x * kWaves) {
     const unsigned stripe = sh / nsh, i = sh - stripe * nsh;
     const uint64_t base = ptrs[static_cast<size_t>(stripe) * ptr_stride + i];
     uint64_t x = 0, tq = 0;
     if (nblk) {
-      const uint64_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + threadIdx.x;
-      uint64_t h = 0;
-      for (unsigned b = 0; b < nblk; ++b)
-        h = apply_op(lt + (b + 1 == nblk ? ISAL_HIP_CRC64_OP_LAST : ISAL_HIP_CRC64_OP_BLOCK), h) ^
-            pp[static_cast<size_t>(b) * kBlock];
-      red[threadIdx.x] = h;
-      __syncthreads();
-      x = lane_tree(red, lt + ISAL_HIP_CRC64_OP_TREE);
+      const uint64_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + 4 * lane;
+      uint64_t v[4] = {0, 0, 0, 0};
+      for (unsigned b = 0; b < nblk; ++b) {
+        const uint64_t* op = lt + (b + 1 == nblk ? ISAL_HIP_CRC64_OP_LAST : ISAL_HIP_CRC64_OP_BLOCK);
+        const uint4* p4 = reinterpret_cast<const uint4*>(pp + static_cast<size_t>(b) * kBlock);
+        const uint4 a = p4[0], c = p4[1];
+        const uint64_t p[4] = {(static_cast<uint64_t>(a.y) << 32) | a.x, (static_cast<uint64_t>(a.w) << 32) | a.z,
+                               (static_cast<uint64_t>(c.y) << 32) | c.x, (static_cast<uint64_t>(c.w) << 32) | c.z};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = apply_op(op, v[j]) ^ p[j];
+      }
+      x = wave_fold(tree, v);
     }
     if (q) {
-      red[threadIdx.x] = 0;
-      __syncthreads();
-      if (static_cast<int>(threadIdx.x) < q)
-        red[threadIdx.x + kBlock - q] = chunk_crc_bytes(
-            lt + ISAL_HIP_CRC64_CHUNK_TAB, base, static_cast<long long>(nfull) * kTile + threadIdx.x * kVec);
-      __syncthreads();
-      tq = lane_tree(red, lt + ISAL_HIP_CRC64_OP_TREE);
+      uint64_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = static_cast<int>(4 * lane) + j - (kBlock - q);  // tail chunk at this position
+        v[j] = c >= 0 ? chunk_crc_bytes(lt + ISAL_HIP_CRC64_CHUNK_TAB, base,
+                                        static_cast<long long>(nfull) * kTile + static_cast<long long>(c) * kVec)
+                      : 0;
+      }
+      tq = wave_fold(tree, v);
     }
-    if (threadIdx.x == 0) {
+    if (lane == 0) {
       uint64_t s = x;
       if (q) s = apply_op(lt + ISAL_HIP_CRC64_OP_TAIL, s) ^ tq;
       const uint8_t* p = reinterpret_cast<const uint8_t*>(base) + (len - rem);
@@ -740,8 +757,9 @@ extern "C" void FUSED64_PART_FN(ISAL_FUSED64_PART)(
 int launch_combine64(const uint64_t* part, const uint64_t* ptrs, int ptr_stride, int nsh, int len,
                      const isal_hip_crc64_geom& g, int refl, const uint64_t* tabs,
                      uint64_t init_term, uint64_t* out, unsigned nshard, hipStream_t s) {
-  // each combine workgroup copies the 52 KB table set once: cap the grid
-  const unsigned grid = nshard < 2048 ? nshard : 2048;
+  // four shards per workgroup at a time; each workgroup copies the 52 KB
+  // table set once, so the grid is capped at what is resident (3 per CU)
+  const unsigned want = (nshard + 3) / 4, grid = want < 768 ? want : 768;
   if (refl)
     ISAL_LAUNCH(crc64_combine<true>, dim3(grid), dim3(kBlock), 0, s, part, ptrs, ptr_stride,
                        nsh, len, static_cast<unsigned>(g.nblk), static_cast<unsigned>(g.nfull),

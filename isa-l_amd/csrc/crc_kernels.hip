@@ -292,39 +292,51 @@ __global__ __launch_bounds__(kBlock) void crc32c_shards_pre(
 }
 
 // ---------------------------------------------------------------------------
-// Combine: one workgroup per shard (grid-stride). Lane L folds its partials of
-// every block (Horner with the byte tables of x^(8*4096*tt); the last block
-// uses x^(8*4096*nfull_last)), multiplies by W[L] to move them to the shard
-// end, adds its ragged-tile chunk times Ct[L]; the XOR of all lanes plus
-// x^(8*len) * init is crc32_iscsi(shard, len, init).
+// Combine: one wave per shard (grid-stride, four shards per workgroup at a
+// time). Lane l takes lane positions L = 4l .. 4l + 3: it folds their
+// partials of every block (Horner with the byte tables of x^(8*4096*tt); the
+// last block uses x^(8*4096*nfull_last)), multiplies each by W[L] to move it
+// to the shard end, adds the ragged-tile chunk times Ct[L]; the XOR over the
+// wave plus x^(8*len) * init is crc32_iscsi(shard, len, init). (Round 5 ran
+// one 256-lane workgroup per shard with a barrier per shard.)
 // ---------------------------------------------------------------------------
+static_assert(kBlock == 256, "crc32c_combine: 4 lane positions per lane of a 64-lane wave");
 __global__ __launch_bounds__(kBlock) void crc32c_combine(
     const uint32_t* __restrict__ part, const uint32_t* __restrict__ tail,
     const uint32_t* __restrict__ plan, unsigned nblk, int has_tail, unsigned init,
     uint32_t* __restrict__ out, unsigned nsh) {
+  constexpr unsigned kWaves = kBlock / 64;
   __shared__ uint32_t kt[2048];
-  __shared__ uint32_t red[kBlock / 64];
   for (int i = threadIdx.x; i < 2048; i += kBlock) kt[i] = plan[i];
   __syncthreads();
-  const uint32_t wl = plan[2048 + threadIdx.x];
-  const uint32_t cl = plan[2304 + threadIdx.x];
+  const unsigned lane = threadIdx.x & 63;
+  const uint4 wl = reinterpret_cast<const uint4*>(plan + 2048)[lane];
+  const uint4 cl = reinterpret_cast<const uint4*>(plan + 2304)[lane];
   const uint32_t xlen = plan[2560];
-  for (unsigned sh = blockIdx.x; sh < nsh; sh += gridDim.x) {
-    const uint32_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + threadIdx.x;
-    uint32_t h = 0;
+  const uint32_t w4[4] = {wl.x, wl.y, wl.z, wl.w}, c4[4] = {cl.x, cl.y, cl.z, cl.w};
+  const uint32_t iterm = crc_mulmod(init, xlen);
+  for (unsigned sh = blockIdx.x * kWaves + (threadIdx.x >> 6); sh < nsh; sh += gridDim.x * kWaves) {
+    const uint32_t* pp = part + static_cast<size_t>(sh) * nblk * kBlock + 4 * lane;
+    uint32_t h[4] = {0, 0, 0, 0};
     for (unsigned b = 0; b < nblk; ++b) {
       const uint32_t* k4 = (b + 1 == nblk) ? kt + 1024 : kt;
-      h = xor3(k4[h & 0xff], k4[256 + ((h >> 8) & 0xff)], k4[512 + ((h >> 16) & 0xff)]) ^
-          k4[768 + (h >> 24)] ^ pp[static_cast<size_t>(b) * kBlock];
+      const uint4 p = *reinterpret_cast<const uint4*>(pp + static_cast<size_t>(b) * kBlock);
+      const uint32_t pv[4] = {p.x, p.y, p.z, p.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        h[j] = xor3(k4[h[j] & 0xff], k4[256 + ((h[j] >> 8) & 0xff)], k4[512 + ((h[j] >> 16) & 0xff)]) ^
+               k4[768 + (h[j] >> 24)] ^ pv[j];
     }
-    uint32_t v = crc_mulmod(h, wl);
-    if (has_tail) v ^= crc_mulmod(tail[static_cast<size_t>(sh) * kBlock + threadIdx.x], cl);
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v ^= crc_mulmod(h[j], w4[j]);
+    if (has_tail) {
+      const uint4 t = reinterpret_cast<const uint4*>(tail + static_cast<size_t>(sh) * kBlock)[lane];
+      v ^= crc_mulmod(t.x, c4[0]) ^ crc_mulmod(t.y, c4[1]) ^ crc_mulmod(t.z, c4[2]) ^ crc_mulmod(t.w, c4[3]);
+    }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) out[sh] = red[0] ^ red[1] ^ red[2] ^ red[3] ^ crc_mulmod(init, xlen);
-    __syncthreads();
+    if (lane == 0) out[sh] = v ^ iterm;
   }
 }
 
@@ -821,7 +833,8 @@ extern "C" int isal_hip_launch_crc_combine(const uint32_t* d_part, const uint32_
                                            void* stream) {
   if (nsh <= 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const unsigned grid = nsh < 4096 ? static_cast<unsigned>(nsh) : 4096u;
+  const unsigned long long want = (static_cast<unsigned long long>(nsh) + 3) / 4;  // four shards per workgroup
+  const unsigned grid = want < 2048 ? static_cast<unsigned>(want) : 2048u;
   ISAL_LAUNCH(crc32c_combine, dim3(grid), dim3(kBlock), 0, s, d_part, d_tail, d_plan,
                      static_cast<unsigned>(nblk), has_tail, init, out, static_cast<unsigned>(nsh));
   isal_hip_count_launch();
