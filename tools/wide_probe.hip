@@ -27,6 +27,7 @@
 // stripe's shards back to back (0, the layout of the sweeps above).
 //
 //   usage: wide_probe [ITERS] [ROUNDS] [LAYOUT]   one JSON line per (shape, variant)
+//          wide_probe ITERS ROUNDS LAYOUT matrix  the library's default over k x p
 //
 // Build: make -C isa-l_amd wide_probe (includes csrc/ec_kernels.hip).
 #include "../isa-l_amd/csrc/ec_kernels.hip"
@@ -203,8 +204,98 @@ static void ldsx(int P, int V, unsigned grid, const uint64_t* dp, int stride, co
   exit(1);
 }
 
+// matrix mode: the library's default dispatch (product tables uploaded, as a
+// batch does) over k x p shapes of 1 MiB shards, ~14 GiB per launch, in
+// bench.py's layout; bit_exact = the same parity as the library without the
+// product tables (the v_perm kernels, which the GPU suite checks against the
+// oracle).
+static int matrix_main(int iters, int rounds, int layout) {
+  const int ks[] = {4, 6, 8, 10, 12, 16, 20, 24, 32}, ps[] = {1, 2, 3, 4, 5, 6, 7, 8};
+  const int len = 1 << 20;
+  const size_t shard = static_cast<size_t>(len);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int round = 0; round < rounds; ++round)
+  for (int k : ks)
+    for (int p : ps) {
+      const int stride = k + p;
+      const int ns = static_cast<int>((14ull << 30) / (static_cast<unsigned long long>(stride) * shard));
+      uint8_t *d = nullptr, *c = nullptr;
+      // layout 0: one buffer, each stripe's k + p shards back to back (c aliases d)
+      CK(hipMalloc(&d, shard * (layout ? k : stride) * ns));
+      if (layout)
+        CK(hipMalloc(&c, shard * p * ns));
+      else
+        c = d;
+      hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t*>(d),
+                         shard * (layout ? k : stride) * ns / 8, 977ull + k * 31 + p);
+      std::vector<uint64_t> hp(static_cast<size_t>(stride) * ns);
+      for (int st = 0; st < ns; ++st)
+        for (int i = 0; i < stride; ++i)
+          hp[static_cast<size_t>(st) * stride + i] = reinterpret_cast<uint64_t>(
+              layout ? (i < k ? d + (static_cast<size_t>(st) * k + i) * shard
+                              : c + (static_cast<size_t>(st) * p + i - k) * shard)
+                     : (i < k ? d : c) + (static_cast<size_t>(st) * stride + i) * shard);
+      uint64_t* dp = nullptr;
+      CK(hipMalloc(&dp, hp.size() * 8));
+      CK(hipMemcpy(dp, hp.data(), hp.size() * 8, hipMemcpyHostToDevice));
+      std::vector<unsigned char> a(stride * k), g(32 * k * p);
+      gf_gen_rs_matrix(a.data(), stride, k);
+      ec_init_tables(k, p, a.data() + k * k, g.data());
+      std::vector<uint32_t> ht(isal_hip_tables_dwords(k, p) + 1);
+      isal_hip_build_tables(k, p, g.data(), ht.data());
+      isal_hip_encmask em, em0;
+      isal_hip_enc_masks(k, p, g.data(), &em);
+      em0 = em;
+      uint32_t* dt = nullptr;
+      CK(hipMalloc(&dt, ht.size() * 4));
+      CK(hipMemcpy(dt, ht.data(), ht.size() * 4, hipMemcpyHostToDevice));
+      std::vector<uint64_t> hl(isal_hip_ldsx_words(k, p));
+      isal_hip_build_ldsx_tables(k, p, g.data(), hl.data());
+      uint64_t* dl = nullptr;
+      CK(hipMalloc(&dl, hl.size() * 8));
+      CK(hipMemcpy(dl, hl.data(), hl.size() * 8, hipMemcpyHostToDevice));
+      em.ldsx = dl;
+      uint8_t* last = reinterpret_cast<uint8_t*>(hp[static_cast<size_t>(ns - 1) * stride + k]);  // p shards apart by layout
+      std::vector<uint8_t> ref(shard * p), got(shard * p);
+      CK(static_cast<hipError_t>(isal_hip_launch_encode(dp, stride, 0, k, dt, len, k, p, ns, 1, &em0, nullptr)));
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(ref.data(), last, shard * p, hipMemcpyDeviceToHost));
+      CK(hipMemset(last, 0xA5, shard * p));
+      auto go = [&]() {
+        CK(static_cast<hipError_t>(isal_hip_launch_encode(dp, stride, 0, k, dt, len, k, p, ns, 1, &em, nullptr)));
+      };
+      go();
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), last, shard * p, hipMemcpyDeviceToHost));
+      const bool ok = memcmp(ref.data(), got.data(), shard * p) == 0;
+      for (int w = 0; w < 2; ++w) go();
+      CK(hipEventRecord(e0, 0));
+      for (int it = 0; it < iters; ++it) go();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= iters;
+      const double bytes = static_cast<double>(stride) * shard * ns;
+      printf("{\"round\": %d, \"layout\": %d, \"k\": %d, \"p\": %d, \"len\": %d, \"stripes\": %d, \"ms\": %.4f, "
+             "\"frac\": %.4f, \"bit_exact\": %s}\n", round, layout, k, p, len, ns, ms, bytes / ms / 1e6 / 8000.0,
+             ok ? "true" : "false");
+      fflush(stdout);
+      CK(hipFree(d));
+      if (layout) CK(hipFree(c));
+      CK(hipFree(dp));
+      CK(hipFree(dt));
+      CK(hipFree(dl));
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 10;
+  if (argc > 4 && strcmp(argv[4], "matrix") == 0)
+    return matrix_main(iters, argc > 2 ? atoi(argv[2]) : 1, argc > 3 ? atoi(argv[3]) : 1);
   const int rounds = argc > 2 ? atoi(argv[2]) : 2;
   // layout 1 (default): bench.py's — the sources of all stripes in one buffer
   // (stripe s, source j at (s k + j) len), the parity rows in another; layout
