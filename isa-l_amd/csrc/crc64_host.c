@@ -47,6 +47,14 @@ bitrev64(uint64_t x)
         return r;
 }
 
+/* The flavour's polynomial in normal form (x^64 implicit), for crc_cpu.c's
+ * carry-less folding constants. */
+uint64_t
+isal_hip_crc64_poly(int variant)
+{
+        return poly_norm[variant >> 1];
+}
+
 int
 isal_hip_crc64_is_refl(int variant)
 {

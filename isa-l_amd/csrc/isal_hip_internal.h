@@ -333,6 +333,7 @@ typedef struct {
 
 int isal_hip_crc64_is_refl(int variant);
 void isal_hip_crc64_cpu_tables(int variant, uint64_t byte[256], uint64_t slice[8 * 256]);
+uint64_t isal_hip_crc64_poly(int variant);
 
 /* ---- the checksum entry points' CPU route (crc_cpu.c): host buffers --------
  * crc32_iscsi semantics (register starts at init, no inversion) and

@@ -282,13 +282,14 @@ def _crc_lengths():
 def test_crc32_iscsi_host_route_vs_oracle(engine, oracle, monkeypatch, simd):
     """crc32_iscsi / _base (reference include/crc.h:136-150) on host buffers:
     == the oracle's restatement of crc_base.c:205-219 at lengths 0..300 and
-    beyond, misaligned starts, random inits; the SSE4.2 path and (CPU_SIMD=0)
-    the slicing-by-8 tables; the committed reference fixtures."""
+    beyond (every 128-byte fold count with ragged tails from 256 on: the
+    PCLMULQDQ folding, then SSE4.2), misaligned starts, random inits; and
+    (CPU_SIMD=0) the slicing-by-8 tables; the committed reference fixtures."""
     monkeypatch.setenv("ISAL_HIP_CPU_SIMD", simd)
     engine.reload_config()
     rng = np.random.default_rng(5)
     big = fill_bytes((1 << 20) + 64, 77)
-    for n in _crc_lengths():
+    for n in _crc_lengths() + list(range(301, 1400, 13)) + [(1 << 20) - 1, (1 << 20) - 129]:
         off = int(rng.integers(0, 16))
         a = np.ascontiguousarray(big[off: off + n])
         init = int(rng.integers(0, 1 << 32))
@@ -304,15 +305,20 @@ def test_crc32_iscsi_host_route_vs_oracle(engine, oracle, monkeypatch, simd):
     engine.reload_config()
 
 
+@pytest.mark.parametrize("simd", ["1", "0"])
 @pytest.mark.parametrize("variant", range(8))
-def test_crc64_host_route_vs_oracle(engine, oracle, variant):
+def test_crc64_host_route_vs_oracle(engine, oracle, monkeypatch, variant, simd):
     """crc64_<flavour> / _base (reference include/crc64.h:54-163) on host
     buffers: == the oracle's restatement of crc64_base.c at lengths 0..300
-    and beyond, misaligned starts, random inits; chaining
-    crc(crc(init, A), B) == crc(init, A || B); the reference fixtures."""
+    and beyond — every 128-byte fold count with ragged tails from 256 on
+    (the PCLMULQDQ path) — misaligned starts, random inits; (CPU_SIMD=0) the
+    slicing-by-8 tables alone; chaining crc(crc(init, A), B) ==
+    crc(init, A || B); the reference fixtures."""
+    monkeypatch.setenv("ISAL_HIP_CPU_SIMD", simd)
+    engine.reload_config()
     rng = np.random.default_rng(100 + variant)
     big = fill_bytes((1 << 20) + 64, 88)
-    for n in _crc_lengths():
+    for n in _crc_lengths() + list(range(301, 1400, 13)) + [(1 << 20) - 1, (1 << 20) - 129]:
         off = int(rng.integers(0, 16))
         a = np.ascontiguousarray(big[off: off + n])
         init = int(rng.integers(0, 1 << 63)) * 2 + int(rng.integers(0, 2))
@@ -328,3 +334,5 @@ def test_crc64_host_route_vs_oracle(engine, oracle, variant):
         if case["variant"] == variant:
             b = ecutil.crc_fixture_bytes(case)
             assert engine.crc64(variant, int(case["init"]), b, b.size) == int(case["crc"]), case.get("len")
+    monkeypatch.undo()
+    engine.reload_config()
