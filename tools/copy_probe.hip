@@ -92,7 +92,9 @@ __global__ __launch_bounds__(B) void skel_tiles(uint64_t data, uint64_t coding, 
 // rate in GB/s of (K + P) * len * S bytes per pass, or a negative error.
 // use_ptrs: bit 0 the pointer table; bits 8-15 T, tiles per workgroup (1, 2
 // or 4; the xor_gen / pq_gen / C2 shapes only for T > 1); bits 16+ threads per
-// workgroup other than 256 (128, 512 or 1024; xor_gen and C2 only, T = 1).
+// workgroup other than 256 (128, 512 or 1024 for xor_gen and C2; 128 or 512
+// for k20p6 / k20p8, the C4 update (7, 6), decode (10, 3) and pq_gen (10, 2);
+// T = 1).
 // Bytes between consecutive shards beyond len in the pointer table (0: the
 // shards abut, every one len-aligned like bench.py's (S, k, len) tensors):
 // whether the shards' alignment to each other changes the rate.
@@ -114,6 +116,13 @@ extern "C" double skel_probe_gbs(void* data, void* coding, int len, int k, int p
     case 128001004: kern = use_ptrs ? skel_tiles<10, 4, true, 1, 128> : skel_tiles<10, 4, false, 1, 128>; break;
     case 512001004: kern = use_ptrs ? skel_tiles<10, 4, true, 1, 512> : skel_tiles<10, 4, false, 1, 512>; break;
     case 1024001004: kern = use_ptrs ? skel_tiles<10, 4, true, 1, 1024> : skel_tiles<10, 4, false, 1, 1024>; break;
+    case 128000706: kern = use_ptrs ? skel_tiles<7, 6, true, 1, 128> : skel_tiles<7, 6, false, 1, 128>; break;
+    case 128001003: kern = use_ptrs ? skel_tiles<10, 3, true, 1, 128> : skel_tiles<10, 3, false, 1, 128>; break;
+    case 128001002: kern = use_ptrs ? skel_tiles<10, 2, true, 1, 128> : skel_tiles<10, 2, false, 1, 128>; break;
+    case 128002006: kern = use_ptrs ? skel_tiles<20, 6, true, 1, 128> : skel_tiles<20, 6, false, 1, 128>; break;
+    case 512002006: kern = use_ptrs ? skel_tiles<20, 6, true, 1, 512> : skel_tiles<20, 6, false, 1, 512>; break;
+    case 128002008: kern = use_ptrs ? skel_tiles<20, 8, true, 1, 128> : skel_tiles<20, 8, false, 1, 128>; break;
+    case 512002008: kern = use_ptrs ? skel_tiles<20, 8, true, 1, 512> : skel_tiles<20, 8, false, 1, 512>; break;
     case 101001: kern = use_ptrs ? skel_tiles<10, 1, true, 2> : skel_tiles<10, 1, false, 2>; break;
     case 101002: kern = use_ptrs ? skel_tiles<10, 2, true, 2> : skel_tiles<10, 2, false, 2>; break;
     case 101004: kern = use_ptrs ? skel_tiles<10, 4, true, 2> : skel_tiles<10, 4, false, 2>; break;
