@@ -1105,7 +1105,7 @@ def main(argv=None):
                         f"({'P' if p == 1 else 'P+Q'}), {n} B shards x {S} stripes/GPU, device-resident")
         else:
             bytes_per_launch = (1 + 2 * p) * n * S
-            kernel = f"ec_update_v16<{p}>"
+            kernel = f"ec_update_v16<{p}, 128>"  # ec_kernels.hip kUpdBlock
             workload = (f"ec_encode_data_update: fold one source into p={p} parity (k={k}), "
                         f"{n} B shards x {S} stripes/GPU, device-resident")
 

@@ -483,7 +483,7 @@ __device__ __forceinline__ void mad_bytes(const uint64_t* __restrict__ sp, int s
   }
 }
 
-template <int P, int ST = kBufNT>
+template <int P, int ST = kBufNT, int B = kBlock>
 __device__ __forceinline__ void update_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src_idx,
                                              int dst0, const uint32_t* __restrict__ tbl, int len,
                                              unsigned nitems, unsigned tiles) {
@@ -491,7 +491,7 @@ __device__ __forceinline__ void update_items(const uint64_t* __restrict__ ptrs, 
     const unsigned stripe = w / tiles;
     const unsigned tile = w - stripe * tiles;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
-    const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
+    const long long off = static_cast<long long>(tile) * (B * kVec) + threadIdx.x * kVec;
     if (off + kVec <= len) {
       const uint4 x = load16<kBufNT>(sp[src_idx], off, len);
       uint4 d[P];
@@ -561,12 +561,12 @@ __global__ __launch_bounds__(kBlock) void ec_encode_karg4(const isal_hip_karg a,
   karg_done(d, (len & 3) != 0 && blockIdx.x == gridDim.x - 1);
 }
 
-template <int P>
-__global__ __launch_bounds__(kBlock) void ec_update_v16(const uint64_t* __restrict__ ptrs,
-                                                        int ptr_stride, int src_idx, int dst0,
-                                                        const uint32_t* __restrict__ tbl, int len,
-                                                        unsigned nitems, unsigned tiles) {
-  update_items<P>(ptrs, ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
+template <int P, int B = kBlock>
+__global__ __launch_bounds__(B) void ec_update_v16(const uint64_t* __restrict__ ptrs,
+                                                   int ptr_stride, int src_idx, int dst0,
+                                                   const uint32_t* __restrict__ tbl, int len,
+                                                   unsigned nitems, unsigned tiles) {
+  update_items<P, kBufNT, B>(ptrs, ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
 }
 
 // One update call whose pointers (source, then P parity rows) and the source's
@@ -944,6 +944,14 @@ hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
   return hipGetLastError();
 }
 
+// The device update runs 128-lane workgroups (2 KiB tiles): C4 shape (k20 p6,
+// 4 MiB x 64), same box, three interleaved rounds
+// (profiles/r06/r06_update_block_ab.jsonl): 0.600 / 0.599 / 0.598 ms against
+// 0.608 / 0.603 / 0.603 at 256 lanes. The 32 KiB LDS occupancy cap, which
+// lifts the update's memory skeleton by 4-8 % (r06_skel_blocks_c2_c3_c4_pq.jsonl),
+// costs the kernel 8-10 % at either size (0.650-0.665 ms).
+constexpr int kUpdBlock = 128, kUpdTile = kUpdBlock * kVec;
+
 template <int P>
 hipError_t update_pass(const uint64_t* ptrs, int ptr_stride, int src_idx, int dst0,
                        const uint32_t* tbl, int len, unsigned nstripes, bool vec16, hipStream_t s) {
@@ -952,10 +960,13 @@ hipError_t update_pass(const uint64_t* ptrs, int ptr_stride, int src_idx, int ds
   const unsigned nitems = nstripes * tiles;
   // (An occupancy cap through dynamic LDS measured flat at 8 workgroups per
   // CU and 2-9 % slower at 4-6, profiles/r04_update_occupancy_ab.jsonl.)
-  if (vec16)
-    ISAL_LAUNCH(ec_update_v16<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
-                       ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
-  else
+  if (vec16) {
+    // 128-lane workgroups, 2 KiB column tiles (kUpdBlock); the caller splits
+    // launches with update_stripes_per_launch
+    const unsigned t2 = static_cast<unsigned>((static_cast<long long>(len) + kUpdTile - 1) / kUpdTile);
+    ISAL_LAUNCH((ec_update_v16<P, kUpdBlock>), dim3(grid_for(nstripes * t2)), dim3(kUpdBlock), 0, s, ptrs,
+                ptr_stride, src_idx, dst0, tbl, len, nstripes * t2, t2);
+  } else
     ISAL_LAUNCH(ec_update_b1<P>, dim3(grid_for(nitems)), dim3(kBlock), 0, s, ptrs,
                        ptr_stride, src_idx, dst0, tbl, len, nitems, tiles);
   isal_hip_count_launch();
@@ -963,8 +974,8 @@ hipError_t update_pass(const uint64_t* ptrs, int ptr_stride, int src_idx, int ds
 }
 
 // Largest stripe count per launch so that nitems stays below kMaxItems.
-unsigned stripes_per_launch(int len, bool vec16) {
-  const long long span = vec16 ? kTile : kBlock;
+unsigned stripes_per_launch(int len, bool vec16, long long vspan = kTile) {
+  const long long span = vec16 ? vspan : kBlock;
   const long long tiles = (static_cast<long long>(len) + span - 1) / span;
   const long long n = static_cast<long long>(kMaxItems) / (tiles ? tiles : 1);
   return static_cast<unsigned>(n > 0 ? n : 1);
@@ -1256,7 +1267,7 @@ extern "C" int isal_hip_launch_update(const uint64_t* d_ptrs, int ptr_stride, in
                                       int vec_i, long long nstripes, int vec16, void* stream) {
   if (len <= 0 || rows <= 0 || nstripes <= 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const unsigned per = stripes_per_launch(len, vec16 != 0);
+  const unsigned per = stripes_per_launch(len, vec16 != 0, kUpdTile);
   for (long long s0 = 0; s0 < nstripes; s0 += per) {
     const unsigned ns = static_cast<unsigned>(nstripes - s0 < per ? nstripes - s0 : per);
     const uint64_t* ptrs = d_ptrs + s0 * ptr_stride;
