@@ -252,8 +252,8 @@ def enc_kernel(rows: int, k: int, coef) -> str:
     4 slots per wave, table halves from LDS; ISAL_HIP_ENC_GLDS=0 off) unless
     they look their products up in LDS product tables (ec_encode_ldsx: 7-8
     rows, or 5-6 rows over k >= 16, k <= 64; ISAL_HIP_ENC_LDSX=1 every 4-8
-    row pass, =0 off). The library names the same instantiation on stderr with
-    ISAL_HIP_LOG=2."""
+    row pass, =0 off). Passes of 1-2 rows run 128-lane workgroups. The library
+    names the same instantiation on stderr with ISAL_HIP_LOG=2."""
     import numpy as np
 
     c = np.asarray(coef, dtype=np.uint8).reshape(rows, k)
@@ -271,8 +271,10 @@ def enc_kernel(rows: int, k: int, coef) -> str:
     if lds == "1" or (lds != "0" and rows - (fl & 1) > 4
                       and (rows <= 6 or (enc_group(k, rows) == 5 and wide5))):  # ec_kernels.hip enc_lds
         fl |= 2
-    # rocprofv3 prints every template argument, the variant's default 0 too
-    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, 2, 2, 2>, {fl}>"
+    # rocprofv3 prints every template argument, the variant's default 0 too;
+    # passes of 1-2 rows run 128-lane workgroups (ec_kernels.hip enc_block)
+    lanes = ", 128" if rows <= 2 else ""
+    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, 2, 2, 2>, {fl}{lanes}>"
 
 
 def copy_ceiling(dev, nbytes: int = 2 << 30, reps: int = 10) -> dict:

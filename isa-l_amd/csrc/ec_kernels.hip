@@ -63,21 +63,21 @@ struct EncOrder<2> {
 };
 
 // The work items of an encode launch: (stripe, 4 KiB column tile) pairs.
-template <int P, class Pol, int FL>
+template <int P, class Pol, int FL, int B = kBlock>
 __device__ __forceinline__ void encode_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
                                              int dst0, const uint32_t* __restrict__ tbl, int len, int k,
                                              unsigned nitems, unsigned tiles, unsigned long long r0m,
                                              unsigned c0m) {
   extern __shared__ uint2 enc_lt[];  // kEncLds: {a0, b0} of every coefficient of the pass
   if constexpr ((FL & kEncLds) != 0) {
-    for (int i = threadIdx.x; i < k * P; i += kBlock) enc_lt[i] = make_uint2(tbl[i * kTbl], tbl[i * kTbl + 2]);
+    for (int i = threadIdx.x; i < k * P; i += B) enc_lt[i] = make_uint2(tbl[i * kTbl], tbl[i * kTbl + 2]);
     __syncthreads();
   }
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
     unsigned stripe, tile;
     EncOrder<Pol::ORDER>::item(w, nitems, tiles, stripe, tile);
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
-    const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
+    const long long off = static_cast<long long>(tile) * (B * kVec) + threadIdx.x * kVec;
     if (off + kVec <= len) {
       uint32_t acc[P][4];
       accum16<P, Pol, FL>(acc, sp + src0, tbl, k, off, len, r0m, c0m, enc_lt);
@@ -91,12 +91,12 @@ __device__ __forceinline__ void encode_items(const uint64_t* __restrict__ ptrs, 
   }
 }
 
-template <int P, class Pol = EncDefault, int FL = kEncLUT>
-__global__ __launch_bounds__(kBlock, (enc_waves<P, Pol::U, FL>())) void ec_encode_v16(
+template <int P, class Pol = EncDefault, int FL = kEncLUT, int B = kBlock>
+__global__ __launch_bounds__(B, (enc_waves<P, Pol::U, FL>())) void ec_encode_v16(
     const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
     const uint32_t* __restrict__ tbl, int len, int k, unsigned nitems, unsigned tiles,
     unsigned long long r0m, unsigned c0m) {
-  encode_items<P, Pol, FL>(ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+  encode_items<P, Pol, FL, B>(ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
 }
 
 // End of a kernel-argument call (isal_hip_kdone): the calling
@@ -841,35 +841,54 @@ size_t enc_lds_alloc(size_t used, int P) {
 // ISAL_HIP_LOG=2: name each vector encode launch the way rocprofv3 prints it
 // (bench.py's roofline.kernel must name the same instantiation;
 // test_bench_kernel_label_matches_launch).
-template <int P, class Pol, int FL>
+template <int P, class Pol, int FL, int B>
 void log_launch() {
-  if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2)
+  if (isal_hip_knob(ISAL_HIP_KNOB_LOG) < 2) return;
+  if (B == kBlock)
     fprintf(stderr, "isal_hip: kernel ec_encode_v16<%d, EncPol<%d, %d, %d, %d>, %d>\n", P, Pol::U, Pol::LD, Pol::ST,
             Pol::ORDER, FL);
+  else
+    fprintf(stderr, "isal_hip: kernel ec_encode_v16<%d, EncPol<%d, %d, %d, %d>, %d, %d>\n", P, Pol::U, Pol::LD,
+            Pol::ST, Pol::ORDER, FL, B);
 }
 
+// Lanes per vector-encode workgroup: 128 (2 KiB tiles) for passes of 1-2
+// rows, 256 otherwise. Same box, three interleaved rounds, ms per launch
+// (profiles/r06/r06_v16_block_ab.jsonl), both with the 32 KiB occupancy cap:
+// xor_gen 1.955 / 1.951 / 1.950 at 128 against 1.979 / 1.978 / 1.972 at 256,
+// pq_gen 2.110 / 2.112 / 2.116 against 2.137 / 2.134 / 2.129. For 3-4 rows
+// 128 lanes lose 1-2 % under that cap (C2 2.449-2.456 vs 2.393-2.401) and
+// tie under a 16 KiB one (the same 20 waves per CU as 256 lanes: C2 2.388 /
+// 2.396 / 2.388, decode 2.300 / 2.302 / 2.314 vs 2.306 / 2.306 / 2.316).
+template <int P>
+constexpr int enc_block() {
+  return P <= 2 ? 128 : kBlock;
+}
+constexpr long long kEncMinSpan = 128 * kVec;  // the smallest tile any encode pass uses
+
 template <int P, int U, int FL>
-void launch_fl(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
-               const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles, unsigned long long r0m,
-               unsigned c0m) {
-  log_launch<P, EncPol<U, kBufNT, kBufNT, 2>, FL>();
+void launch_fl(hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0, const uint32_t* tbl,
+               int len, int k, unsigned nstripes, unsigned long long r0m, unsigned c0m) {
+  constexpr int B = enc_block<P>();
+  log_launch<P, EncPol<U, kBufNT, kBufNT, 2>, FL, B>();
+  const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + B * kVec - 1) / (B * kVec));
+  const unsigned nitems = nstripes * tiles;
   const size_t lds = enc_lds_alloc((FL & kEncLds) ? lds_bytes<P>(k) : 0, P);
-  ISAL_LAUNCH((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, FL>), dim3(grid), dim3(kBlock), lds, s,
-                     ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+  ISAL_LAUNCH((ec_encode_v16<P, EncPol<U, kBufNT, kBufNT, 2>, FL, B>), dim3(grid_for(nitems)), dim3(B), lds, s,
+              ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
 }
 
 template <int P, int U>
-void launch_v16(unsigned grid, hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0,
-                int dst0, const uint32_t* tbl, int len, int k, unsigned nitems, unsigned tiles,
-                bool x, unsigned long long r0m, unsigned c0m) {
+void launch_v16(hipStream_t s, const uint64_t* ptrs, int ptr_stride, int src0, int dst0, const uint32_t* tbl,
+                int len, int k, unsigned nstripes, bool x, unsigned long long r0m, unsigned c0m) {
   if (enc_lds(P, x, U) && x)
-    launch_fl<P, U, kEncXor | kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+    launch_fl<P, U, kEncXor | kEncLds>(s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nstripes, r0m, c0m);
   else if (enc_lds(P, x, U))
-    launch_fl<P, U, kEncLds>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
+    launch_fl<P, U, kEncLds>(s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nstripes, 0ull, 0u);
   else if (x)
-    launch_fl<P, U, kEncXor>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
+    launch_fl<P, U, kEncXor>(s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nstripes, r0m, c0m);
   else
-    launch_fl<P, U, kEncLUT>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, 0ull, 0u);
+    launch_fl<P, U, kEncLUT>(s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nstripes, 0ull, 0u);
 }
 
 // Passes of 7-8 rows over at most kLdsxMaxK sources take the LDS product
@@ -928,13 +947,13 @@ hipError_t encode_pass(const uint64_t* ptrs, int ptr_stride, int src0, int dst0,
     launch_glds_r<P>(x, grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, r0m, c0m);
   } else if (vec16) {
     switch (enc_group(k, P)) {
-#define EC_GROUP(u)                                                                                   \
-  case u:                                                                                             \
-    launch_v16<P, u>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, x, r0m, c0m); \
+#define EC_GROUP(u)                                                                          \
+  case u:                                                                                    \
+    launch_v16<P, u>(s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nstripes, x, r0m, c0m);  \
     break;
       EC_GROUP(12) EC_GROUP(10) EC_GROUP(8) EC_GROUP(6) EC_GROUP(5)
 #undef EC_GROUP
-      default: launch_v16<P, 4>(grid, s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nitems, tiles, x, r0m, c0m); break;
+      default: launch_v16<P, 4>(s, ptrs, ptr_stride, src0, dst0, tbl, len, k, nstripes, x, r0m, c0m); break;
     }
   } else {
     ISAL_LAUNCH(ec_encode_b1<P>, dim3(grid), dim3(kBlock), 0, s, ptrs, ptr_stride, src0,
@@ -962,7 +981,7 @@ hipError_t update_pass(const uint64_t* ptrs, int ptr_stride, int src_idx, int ds
   // CU and 2-9 % slower at 4-6, profiles/r04_update_occupancy_ab.jsonl.)
   if (vec16) {
     // 128-lane workgroups, 2 KiB column tiles (kUpdBlock); the caller splits
-    // launches with update_stripes_per_launch
+    // launches with stripes_per_launch(len, true, kUpdTile)
     const unsigned t2 = static_cast<unsigned>((static_cast<long long>(len) + kUpdTile - 1) / kUpdTile);
     ISAL_LAUNCH((ec_update_v16<P, kUpdBlock>), dim3(grid_for(nstripes * t2)), dim3(kUpdBlock), 0, s, ptrs,
                 ptr_stride, src_idx, dst0, tbl, len, nstripes * t2, t2);
@@ -997,7 +1016,7 @@ extern "C" int isal_hip_launch_encode(const uint64_t* d_ptrs, int ptr_stride, in
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint64_t* ldsx_all = em ? em->ldsx : nullptr;
   em = enc_xor_masks(em);
-  const unsigned per = stripes_per_launch(len, vec16 != 0);
+  const unsigned per = stripes_per_launch(len, vec16 != 0, kEncMinSpan);
   for (long long s0 = 0; s0 < nstripes; s0 += per) {
     const unsigned ns = static_cast<unsigned>(nstripes - s0 < per ? nstripes - s0 : per);
     const uint64_t* ptrs = d_ptrs + s0 * ptr_stride;

@@ -1854,6 +1854,10 @@ def test_bench_rccl_control_plane_single_rank(gpu):
     (["--k", "10", "--p", "8"], {"ISAL_HIP_ENC_GLDS": "0", "ISAL_HIP_ENC_LDSX": "0"}),  # 8 rows through registers
     (["--k", "7", "--p", "5"], {"ISAL_HIP_ENC_XOR": "0", "ISAL_HIP_ENC_LDSX": "0"}),     # LDS-DMA ring, lookups only
     (["--workload", "decode"], {}),
+    (["--k", "10", "--p", "2"], {}),                                  # 2 rows: 128-lane workgroups
+    (["--k", "12", "--p", "1"], {"ISAL_HIP_ENC_XOR": "0"}),           # 1 row, lookups: 128 lanes
+    (["--workload", "pq_gen"], {}),
+    (["--workload", "xor_gen"], {}),
 ])
 def test_bench_kernel_label_matches_launch(gpu, args, env):
     """bench.py's roofline.kernel (the name its PMC / steady-state profile files

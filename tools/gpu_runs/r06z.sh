@@ -3,7 +3,7 @@
 # trace and HBM-traffic passes, converted into profiles/r06/ (tools/profile_import.py),
 # then its bench line, which cites those files. PART=a: GPU suite, smoke, C2 headline
 # (with the CPU baseline); PART=b/c: the other workloads; PART=d: the C4 update again
-# after its kernel changed.
+# after its kernel changed; PART=e: full suite, smoke and the RAID-gen lines after theirs did.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -35,6 +35,13 @@ elif [ $PART = b ]; then
   one k16p8 encode --k 16 --p 8 --len 1048576 --stripes 512 || exit 1
   one k20p6 encode --k 20 --p 6 --len 4194304 --stripes 64 || exit 1
   one k20p8 encode --k 20 --p 8 --len 4194304 --stripes 64 || exit 1
+elif [ $PART = e ]; then  # after the 128-lane encode for 1-2 row passes: full suite, smoke, RAID-gen lines
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -60 $O/pytest.txt; exit 1; }
+  tail -3 $O/pytest.txt
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { cat $O/smoke.txt; exit 1; }
+  tail -1 $O/smoke.txt
+  one pq_gen pq_gen || exit 1
+  one xor_gen xor_gen || exit 1
 elif [ $PART = d ]; then  # after the 128-lane update kernel
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "update or selftest or c4 or pipe" > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
   tail -1 $O/pytest.txt
