@@ -472,6 +472,40 @@ _KARG_SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_batch_encode_random_shapes_vs_oracle(engine, oracle, gpu, seed):
+    """Randomized shapes through the batch encode, whatever kernel the
+    library's dispatch picks for each pass (v16 at 128 or 256 lanes, the
+    LDS-DMA ring, the LDS product tables, byte lanes for ragged tails): k in
+    1..64, rows in 1..16 (several passes), any len up to ~40 KiB, random,
+    0/1-structured or Vandermonde coefficients; every parity byte == oracle."""
+    import torch
+
+    rng = np.random.default_rng(7000 + seed)
+    for _ in range(12):
+        k = int(rng.integers(1, 65))
+        rows = int(rng.integers(1, 17))
+        n = int(rng.choice([int(rng.integers(1, 4096)), int(rng.integers(4096, 40960)),
+                            4096 * int(rng.integers(1, 10))]))
+        ns = int(rng.integers(1, 4))
+        kind = str(rng.choice(["rs", "mask", "big"]))
+        if kind == "rs" and k + rows <= 255:
+            coef = engine.gf_gen_rs_matrix(k + rows, k)[k * k:]
+        else:
+            coef = _coef_01(rng, k, rows, "mask" if kind == "mask" else "big")
+        tbls = engine.ec_init_tables(k, rows, coef)
+        data, coding, dptr, cptr = _stripes(torch, gpu, ns, k, rows, n, int(rng.integers(1, 1 << 30)))
+        b = engine.Batch(n, k, rows, tbls, ns, dptr, cptr)
+        b.encode(0)
+        torch.cuda.synchronize()
+        h_data, h_cod = _host(data), _host(coding)
+        want = _oracle_encode_all(oracle, coef, k, rows, [[h_data[s, j] for j in range(k)] for s in range(ns)])
+        for s in range(ns):
+            for l in range(rows):
+                assert np.array_equal(h_cod[s, l], want[s][l]), (k, rows, n, ns, kind, s, l)
+        b.close()
+
+
 @pytest.mark.parametrize("narrow,k,rows,n", [(w,) + s for w in ("1", "0") for s in _KARG_SHAPES] + [
     ("", 10, 4, 1 << 20),         # default threshold: the last 4-byte-lane size
     ("", 10, 4, (1 << 20) + 16),  # one lane past it: the 16-byte-lane kernel
