@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the R06_* switch this script sets existed only in the experiment's working tree (removed after
+# the A/B; the shipped library ignores it), so re-running it today times the shipped kernel in every arm.
 # r06aa: device update (C4 shape) with 128-thread workgroups and/or the 32 KiB LDS occupancy cap
 # (R06_UPD=128 / 128c / 256c) against the shipped 256 threads, no cap; parity tests under 128c;
 # three interleaved rounds.

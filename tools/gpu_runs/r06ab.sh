@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the R06_* switch this script sets existed only in the experiment's working tree (removed after
+# the A/B; the shipped library ignores it), so re-running it today times the shipped kernel in every arm.
 # r06ab: the v16 encode (passes of <= 4 rows) with 128-lane workgroups (2 KiB tiles) under a
 # 32 KiB (R06_V16_B=128) or 16 KiB (128h) LDS occupancy cap, against the shipped 256 lanes /
 # 32 KiB: parity tests under 128, then C2 / C3 decode / pq_gen / xor_gen lines, three interleaved

@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the R06_* switch this script sets existed only in the experiment's working tree (removed after
+# the A/B; the shipped library ignores it), so re-running it today times the shipped kernel in every arm.
 # r06v: fused encode + CRC64 at C2: 512-lane workgroups sharing one table copy forced to 4 waves
 # per SIMD (128 VGPRs, 14 spilled; R06_FUSED_NV=2) against the shipped 256-lane, 3-wave kernel
 # (=1), three interleaved rounds, same box; CRC64 fused tests under both.

@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the R06_* switch this script sets existed only in the experiment's working tree (removed after
+# the A/B; the shipped library ignores it), so re-running it today times the shipped kernel in every arm.
 # r06y: ec_encode_ldsx with 128-thread workgroups (2 KiB tiles; R06_LDSX_B=128) against 256
 # (4 KiB, shipped): parity tests with the tables forced under 128, then bench lines, two
 # interleaved rounds.
