@@ -661,7 +661,7 @@ __device__ __forceinline__ void ldsx_acc(Acc64 (&acc)[16], const uint4& x, uint3
 
 // transpose the 16 accumulators into the P rows' 16 bytes and store them: row
 // l, dword d = byte l of acc[4d .. 4d + 3] (rows 0-3 in .lo, 4-7 in .hi)
-template <int P>
+template <int P, int ST = kBufNT>
 __device__ __forceinline__ void ldsx_store(const Acc64 (&acc)[16], const uint64_t* __restrict__ sp, int dst0,
                                            long long off, int len) {
   uint32_t out[P][4];
@@ -683,14 +683,13 @@ __device__ __forceinline__ void ldsx_store(const Acc64 (&acc)[16], const uint64_
   }
 #pragma unroll
   for (int l = 0; l < P; ++l)
-    store16<kBufNT>(sp[dst0 + l], off, make_uint4(out[l][0], out[l][1], out[l][2], out[l][3]), len);
+    store16<ST>(sp[dst0 + l], off, make_uint4(out[l][0], out[l][1], out[l][2], out[l][3]), len);
 }
 
-template <int P, int U>
-__global__ __launch_bounds__(kBlock) void ec_encode_ldsx(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
-                                                         int dst0, const uint32_t* __restrict__ tbl,
-                                                         const uint64_t* __restrict__ ltg, int len, int k,
-                                                         unsigned nitems, unsigned tiles) {
+template <int P, int U, int ST>
+__device__ __forceinline__ void ldsx_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
+                                           const uint32_t* __restrict__ tbl, const uint64_t* __restrict__ ltg,
+                                           int len, int k, unsigned nitems, unsigned tiles) {
   extern __shared__ uint64_t ldsx_t[];  // [k][32] T5, then [k][8] T3
   for (int i = threadIdx.x; i < k * ISAL_HIP_LDSX_ENTRIES; i += kBlock) ldsx_t[i] = ltg[i];
   __syncthreads();
@@ -725,8 +724,30 @@ __global__ __launch_bounds__(kBlock) void ec_encode_ldsx(const uint64_t* __restr
 #pragma unroll
       for (int u = 0; u < U; ++u) a[u] = b[u];
     }
-    ldsx_store<P>(acc, sp, dst0, off, len);
+    ldsx_store<P, ST>(acc, sp, dst0, off, len);
   }
+}
+
+template <int P, int U>
+__global__ __launch_bounds__(kBlock) void ec_encode_ldsx(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0,
+                                                         int dst0, const uint32_t* __restrict__ tbl,
+                                                         const uint64_t* __restrict__ ltg, int len, int k,
+                                                         unsigned nitems, unsigned tiles) {
+  ldsx_items<P, U, kBufNT>(ptrs, ptr_stride, src0, dst0, tbl, ltg, len, k, nitems, tiles);
+}
+
+// The drop-in call's single stripe through the LDS product tables (a wide
+// pass of 7-8 rows; the thread's table cache uploads them, isal_hip_shim.c):
+// pointers and v_perm tables (for the ragged tail) as kernel arguments, the
+// parity stored write-through and completed through the mailbox as
+// ec_encode_karg.
+template <int P>
+__global__ __launch_bounds__(kBlock) void ec_encode_karg_ldsx(const isal_hip_karg a, const isal_hip_kdone d,
+                                                              const uint64_t* __restrict__ ltg, int len, int k,
+                                                              unsigned tiles) {
+  const isal_hip_karg* ka = (const isal_hip_karg*)__builtin_amdgcn_kernarg_segment_ptr();
+  ldsx_items<P, 2, kBufSC1NT>(ka->ptrs, k + P, 0, k, ka->tbl, ltg, len, k, tiles, tiles);
+  karg_done(d, (len & (kVec - 1)) != 0 && blockIdx.x == gridDim.x - 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1068,8 +1089,23 @@ static bool karg_narrow(int len, int busy) {
 
 static const isal_hip_kdone kNoDone = {nullptr, nullptr, nullptr, 0ull};
 
+// Drop-in encodes of 7-8 rows over at most 12 sources take the LDS product
+// tables too, unless ISAL_HIP_ENC_LDSX=0 (with 4-byte lanes, under 12+ calls
+// in flight, they keep v_perm). One synchronous call per 1 MiB stripe, two
+// interleaved rounds, same box (profiles/r06/r06_dropin_ldsx_ab.txt): k10 p8
+// 17.6 / 19.8 us against 19.6 / 21.0 with v_perm, k10 p7 17.9 / 18.5 against
+// 19.3 / 19.0; k20 p8 30.1 / 29.7 against 29.7 / 28.5 — each workgroup loads
+// its k x 320 B of tables before the first source, which a single stripe's
+// latency feels as k grows.
+constexpr int kKargLdsxMaxK = 12;
+extern "C" int isal_hip_karg_ldsx(int k, int rows) {
+  return rows >= kLdsxAutoRows && rows <= EC_MAX_ROWS_PER_PASS && k >= 1 && k <= kKargLdsxMaxK &&
+         isal_hip_knob(ISAL_HIP_KNOB_ENC_LDSX) != 0;
+}
+
 extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, const isal_hip_kdone* d, int len, int k,
-                                           int rows, const isal_hip_encmask* em, int busy, void* stream) {
+                                           int rows, const isal_hip_encmask* em, int busy, const uint64_t* ldsx,
+                                           void* stream) {
   if (!d) d = &kNoDone;
   if (len <= 0 || rows <= 0) return 0;
   if (rows > EC_MAX_ROWS_PER_PASS || k + rows > ISAL_HIP_KARG_PTRS ||
@@ -1077,6 +1113,19 @@ extern "C" int isal_hip_launch_encode_karg(const isal_hip_karg* a, const isal_hi
     return static_cast<int>(hipErrorInvalidValue);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool narrow = karg_narrow(len, busy);
+  if (!narrow && isal_hip_karg_ldsx(k, rows) && ldsx) {  // 16-byte lanes on the product tables
+    const unsigned tiles = static_cast<unsigned>((static_cast<long long>(len) + kTile - 1) / kTile);
+    const size_t lds = static_cast<size_t>(k) * ISAL_HIP_LDSX_ENTRIES * 8;
+    if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2) fprintf(stderr, "isal_hip: kernel ec_encode_karg_ldsx<%d>\n", rows);
+    switch (rows) {
+      case 7: ISAL_LAUNCH(ec_encode_karg_ldsx<7>, dim3(tiles), dim3(kBlock), lds, s, *a, *d, ldsx, len, k, tiles); break;
+      case 8: ISAL_LAUNCH(ec_encode_karg_ldsx<8>, dim3(tiles), dim3(kBlock), lds, s, *a, *d, ldsx, len, k, tiles); break;
+      default: return static_cast<int>(hipErrorInvalidValue);
+    }
+    isal_hip_count_launch();
+    return static_cast<int>(hipGetLastError());
+  }
+
   if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2)
     fprintf(stderr, "isal_hip: kernel %s<%d>\n", narrow ? "ec_encode_karg4" : "ec_encode_karg", rows);
   if (narrow) {

@@ -237,8 +237,9 @@ isal_hip_ldsx_words(int k, int rows)
         return (size_t) passes * (size_t) k * ISAL_HIP_LDSX_ENTRIES;
 }
 
-void
-isal_hip_build_ldsx_tables(int k, int rows, const unsigned char *gftbls, uint64_t *out)
+/* coefficient (r, j) at c[(r * k + j) * stride + off] */
+static void
+ldsx_build(int k, int rows, const unsigned char *c, int stride, int off, uint64_t *out)
 {
         int r0, j, l, v;
         for (r0 = 0; r0 < rows; r0 += EC_MAX_ROWS_PER_PASS) {
@@ -248,14 +249,27 @@ isal_hip_build_ldsx_tables(int k, int rows, const unsigned char *gftbls, uint64_
                 memset(t5, 0, (size_t) k * ISAL_HIP_LDSX_ENTRIES * 8);
                 for (j = 0; j < k; j++)
                         for (l = 0; l < P; l++) {
-                                const unsigned char c = gftbls[((size_t) (r0 + l) * k + j) * 32 + 1];
+                                const unsigned char cf = c[((size_t) (r0 + l) * k + j) * stride + off];
                                 for (v = 0; v < 32; v++)
-                                        t5[(size_t) j * 32 + v] |= (uint64_t) gf_mul(c, (unsigned char) v) << (8 * l);
+                                        t5[(size_t) j * 32 + v] |= (uint64_t) gf_mul(cf, (unsigned char) v) << (8 * l);
                                 for (v = 0; v < 8; v++)
-                                        t3[(size_t) j * 8 + v] |= (uint64_t) gf_mul(c, (unsigned char) (v << 5))
+                                        t3[(size_t) j * 8 + v] |= (uint64_t) gf_mul(cf, (unsigned char) (v << 5))
                                                                   << (8 * l);
                         }
         }
+}
+
+void
+isal_hip_build_ldsx_tables(int k, int rows, const unsigned char *gftbls, uint64_t *out)
+{
+        ldsx_build(k, rows, gftbls, 32, 1, out);
+}
+
+/* The same from the rows x k coefficient bytes themselves. */
+void
+isal_hip_build_ldsx_tables_coef(int k, int rows, const unsigned char *coef, uint64_t *out)
+{
+        ldsx_build(k, rows, coef, 1, 0, out);
 }
 
 void

@@ -71,6 +71,7 @@ void isal_hip_enc_masks(int k, int rows, const unsigned char *gftbls, isal_hip_e
 #define ISAL_HIP_LDSX_ENTRIES 40
 size_t isal_hip_ldsx_words(int k, int rows);
 void isal_hip_build_ldsx_tables(int k, int rows, const unsigned char *gftbls, uint64_t *out);
+void isal_hip_build_ldsx_tables_coef(int k, int rows, const unsigned char *coef, uint64_t *out);
 
 /* Kernel launchers (ec_kernels.hip). Return 0 or a hipError_t value.
  * `stream` is a hipStream_t. `vec16` = every shard address is 16-byte aligned. */
@@ -114,7 +115,10 @@ typedef struct {
 /* busy: kernel-argument calls of this process in flight, this one included
  * (chooses the lane width, ec_kernels.hip karg_narrow). */
 int isal_hip_launch_encode_karg(const isal_hip_karg *a, const isal_hip_kdone *d, int len, int k, int rows,
-                                const isal_hip_encmask *em, int busy, void *stream);
+                                const isal_hip_encmask *em, int busy, const uint64_t *ldsx, void *stream);
+/* whether a drop-in encode of this shape runs on LDS product tables (then the
+ * caller passes them to isal_hip_launch_encode_karg; NULL keeps v_perm) */
+int isal_hip_karg_ldsx(int k, int rows);
 /* ec_encode_data_update of one stripe the same way: ptrs = {source, rows
  * parity}, tbl = the source's tables for rows <= EC_MAX_ROWS_PER_PASS outputs. */
 int isal_hip_launch_update_karg(const isal_hip_karg *a, const isal_hip_kdone *d, int len, int rows,

@@ -274,6 +274,11 @@ typedef struct {
         uint32_t *ttbl;
         size_t tcap_coef, tcap_tbl;
         isal_hip_encmask tem;
+        /* the same coefficients' LDS product tables on the device (drop-in
+         * encodes of 7-8 rows, isal_hip_karg_ldsx), built on first use */
+        uint64_t *d_ldsx;
+        size_t ldsx_cap;
+        int ldsx_ok;
         /* completion of kernel-argument calls (isal_hip_kdone): device words
          * {arrival counter, verify result}, the page-locked host mailbox
          * {seq, result} and its device view, the last sequence number, and
@@ -388,6 +393,8 @@ ctx_free(ctx_t *c)
                         (void) hipFree(c->c64[v].d_tabs);
         if (c->d_cpart)
                 (void) hipFree(c->d_cpart);
+        if (c->d_ldsx)
+                (void) hipFree(c->d_ldsx);
         free(c->jobs);
         free(c->tcoef);
         free(c->ttbl);
@@ -500,6 +507,7 @@ ctx_tables(ctx_t *c, int k, int rows, const unsigned char *gftbls, const isal_hi
                         c->tcap_tbl = cap;
                 }
                 c->tk = -1; /* not valid until rebuilt */
+                c->ldsx_ok = 0;
                 for (i = 0; i < n; i++)
                         c->tcoef[i] = gftbls[i * 32 + 1];
                 isal_hip_build_tables(k, rows, gftbls, c->ttbl);
@@ -1652,6 +1660,38 @@ wait_done(ctx_t *c, unsigned long long seq)
         return hipSuccess;
 }
 
+/* The LDS product tables of the thread's cached coefficients (ctx_tables) on
+ * the device, uploaded when the coefficients change; NULL (the call then
+ * keeps the v_perm kernel) when memory runs out. The upload is synchronous and
+ * no kernel of this context is in flight: every drop-in call has completed
+ * before the next one starts. */
+static const uint64_t *
+ctx_ldsx(ctx_t *c, int k, int rows)
+{
+        const size_t nw = isal_hip_ldsx_words(k, rows);
+        uint64_t *h;
+        if (c->ldsx_ok)
+                return c->d_ldsx;
+        if (nw > c->ldsx_cap) {
+                if (c->d_ldsx)
+                        (void) hipFree(c->d_ldsx);
+                c->d_ldsx = NULL;
+                c->ldsx_cap = 0;
+                if (hipMalloc((void **) &c->d_ldsx, nw * 8) != hipSuccess) {
+                        c->d_ldsx = NULL;
+                        return NULL;
+                }
+                c->ldsx_cap = nw;
+        }
+        if (!(h = (uint64_t *) malloc(nw * 8)))
+                return NULL;
+        isal_hip_build_ldsx_tables_coef(k, rows, c->tcoef, h);
+        if (hipMemcpy(c->d_ldsx, h, nw * 8, hipMemcpyHostToDevice) == hipSuccess)
+                c->ldsx_ok = 1;
+        free(h);
+        return c->ldsx_ok ? c->d_ldsx : NULL;
+}
+
 /* A kernel-argument call's arguments, in the 2 KiB block the kernels read
  * from their kernarg segment. mail: the completion mailbox is used (every
  * shard is hipMalloc memory: managed memory the host may read directly is
@@ -1697,9 +1737,12 @@ gpu_karg(ctx_t *c, int op, int len, int k, int rows, int vec_i, const uint64_t *
         } else {
                 memcpy(a.tbl, tbl, isal_hip_tables_dwords(k, rows) * 4);
                 busy = __atomic_add_fetch(&inflight, 1, __ATOMIC_RELAXED);
-                e = (hipError_t) (op == OP_VERIFY ? isal_hip_launch_verify_karg(&a, &d, len, k, rows, em, c->stream)
-                                                  : isal_hip_launch_encode_karg(&a, &d, len, k, rows, em, busy,
-                                                                                c->stream));
+                e = (hipError_t) (op == OP_VERIFY
+                                          ? isal_hip_launch_verify_karg(&a, &d, len, k, rows, em, c->stream)
+                                          : isal_hip_launch_encode_karg(
+                                                    &a, &d, len, k, rows, em, busy,
+                                                    isal_hip_karg_ldsx(k, rows) ? ctx_ldsx(c, k, rows) : NULL,
+                                                    c->stream));
         }
         if (e == hipSuccess) {
                 r.what = wait_what[op];

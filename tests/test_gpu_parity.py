@@ -469,6 +469,9 @@ _KARG_SHAPES = [
     (10, 8, 4096 + 4),     # 8 rows
     (1, 1, 64),
     (14, 6, 20000),        # 5 * k * rows = 420 of the 448 table dwords
+    (11, 8, 8192 + 100),   # 8 rows on the LDS product tables, k at the table limit, ragged
+    (2, 7, 48),            # product tables, k below the load pair, three lanes
+    (9, 7, 4096 + 16),     # product tables, odd k, one lane into the second tile
 ]
 
 
@@ -540,7 +543,9 @@ def test_dropin_kernel_args_vs_oracle(engine, oracle, gpu, monkeypatch, capfd, n
     err = capfd.readouterr().err
     assert "kernel-args" in err
     four = narrow == "1"  # default, one call in flight: 16-byte lanes
-    assert f"kernel {'ec_encode_karg4' if four else 'ec_encode_karg'}<{rows}>" in err, err
+    # 16-byte lanes over 7-8 rows take the LDS product tables (isal_hip_karg_ldsx)
+    name = "ec_encode_karg4" if four else "ec_encode_karg_ldsx" if rows >= 7 and k <= 12 else "ec_encode_karg"
+    assert f"kernel {name}<{rows}>" in err, err
     out = _host(buf)
     for l in range(rows):
         base = (k + l) * stride
