@@ -271,10 +271,11 @@ def enc_kernel(rows: int, k: int, coef) -> str:
     if lds == "1" or (lds != "0" and rows - (fl & 1) > 4
                       and (rows <= 6 or (enc_group(k, rows) == 5 and wide5))):  # ec_kernels.hip enc_lds
         fl |= 2
-    # rocprofv3 prints every template argument, the variant's default 0 too;
-    # passes of 1-2 rows run 128-lane workgroups (ec_kernels.hip enc_block)
-    lanes = ", 128" if rows <= 2 else ""
-    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, 2, 2, 2>, {fl}{lanes}>"
+    # rocprofv3 prints every template argument, defaults included: the
+    # variant's 0 and the lanes per workgroup (128 for passes of 1-2 rows,
+    # ec_kernels.hip enc_block, else 256)
+    lanes = 128 if rows <= 2 else 256
+    return f"ec_encode_v16<{rows}, EncPol<{enc_group(k, rows)}, 2, 2, 2>, {fl}, {lanes}>"
 
 
 def copy_ceiling(dev, nbytes: int = 2 << 30, reps: int = 10) -> dict:

@@ -864,11 +864,7 @@ size_t enc_lds_alloc(size_t used, int P) {
 // test_bench_kernel_label_matches_launch).
 template <int P, class Pol, int FL, int B>
 void log_launch() {
-  if (isal_hip_knob(ISAL_HIP_KNOB_LOG) < 2) return;
-  if (B == kBlock)
-    fprintf(stderr, "isal_hip: kernel ec_encode_v16<%d, EncPol<%d, %d, %d, %d>, %d>\n", P, Pol::U, Pol::LD, Pol::ST,
-            Pol::ORDER, FL);
-  else
+  if (isal_hip_knob(ISAL_HIP_KNOB_LOG) >= 2)
     fprintf(stderr, "isal_hip: kernel ec_encode_v16<%d, EncPol<%d, %d, %d, %d>, %d, %d>\n", P, Pol::U, Pol::LD,
             Pol::ST, Pol::ORDER, FL, B);
 }

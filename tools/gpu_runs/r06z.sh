@@ -3,7 +3,8 @@
 # trace and HBM-traffic passes, converted into profiles/r06/ (tools/profile_import.py),
 # then its bench line, which cites those files. PART=a: GPU suite, smoke, C2 headline
 # (with the CPU baseline); PART=b/c: the other workloads; PART=d: the C4 update again
-# after its kernel changed; PART=e: full suite, smoke and the RAID-gen lines after theirs did.
+# after its kernel changed; PART=e: full suite, smoke and the RAID-gen lines after theirs did;
+# PART=f: the decode line again (kernel name now carries the lane count, as rocprofv3 prints it).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -42,6 +43,8 @@ elif [ $PART = e ]; then  # after the 128-lane encode for 1-2 row passes: full s
   tail -1 $O/smoke.txt
   one pq_gen pq_gen || exit 1
   one xor_gen xor_gen || exit 1
+elif [ $PART = f ]; then  # the decode again after the v16 kernels gained their lane-count template argument
+  one c3 decode || exit 1
 elif [ $PART = d ]; then  # after the 128-lane update kernel
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "update or selftest or c4 or pipe" > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
   tail -1 $O/pytest.txt
