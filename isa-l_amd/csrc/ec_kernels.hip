@@ -686,12 +686,12 @@ __device__ __forceinline__ void ldsx_store(const Acc64 (&acc)[16], const uint64_
     store16<ST>(sp[dst0 + l], off, make_uint4(out[l][0], out[l][1], out[l][2], out[l][3]), len);
 }
 
-template <int P, int U, int ST>
+template <int P, int U, int ST, int B = kBlock>
 __device__ __forceinline__ void ldsx_items(const uint64_t* __restrict__ ptrs, int ptr_stride, int src0, int dst0,
                                            const uint32_t* __restrict__ tbl, const uint64_t* __restrict__ ltg,
                                            int len, int k, unsigned nitems, unsigned tiles) {
   extern __shared__ uint64_t ldsx_t[];  // [k][32] T5, then [k][8] T3
-  for (int i = threadIdx.x; i < k * ISAL_HIP_LDSX_ENTRIES; i += kBlock) ldsx_t[i] = ltg[i];
+  for (int i = threadIdx.x; i < k * ISAL_HIP_LDSX_ENTRIES; i += B) ldsx_t[i] = ltg[i];
   __syncthreads();
   const uint32_t base5 = lds_off(ldsx_t), base3 = base5 + static_cast<uint32_t>(k) * 256u;
   for (unsigned w = blockIdx.x; w < nitems; w += gridDim.x) {
@@ -699,7 +699,7 @@ __device__ __forceinline__ void ldsx_items(const uint64_t* __restrict__ ptrs, in
     const unsigned stripe = v / tiles;
     const unsigned tile = v - stripe * tiles;
     const uint64_t* __restrict__ sp = ptrs + static_cast<size_t>(stripe) * ptr_stride;
-    const long long off = static_cast<long long>(tile) * kTile + threadIdx.x * kVec;
+    const long long off = static_cast<long long>(tile) * (B * kVec) + threadIdx.x * kVec;
     if (off + kVec > len) {
       if (off < len) dot_bytes<P>(sp, src0, dst0, tbl, k, off, static_cast<int>(len - off));
       continue;

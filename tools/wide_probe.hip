@@ -28,6 +28,7 @@
 //
 //   usage: wide_probe [ITERS] [ROUNDS] [LAYOUT]   one JSON line per (shape, variant)
 //          wide_probe ITERS ROUNDS LAYOUT matrix  the library's default over k x p
+//          wide_probe ITERS ROUNDS 1 lanes        the product tables at 256 / 128 lanes x caps
 //
 // Build: make -C isa-l_amd wide_probe (includes csrc/ec_kernels.hip).
 #include "../isa-l_amd/csrc/ec_kernels.hip"
@@ -292,8 +293,115 @@ static int matrix_main(int iters, int rounds, int layout) {
   return 0;
 }
 
+// ec_encode_ldsx's body at 128 lanes (2 KiB tiles)
+template <int P>
+__global__ __launch_bounds__(128) void ldsx_128(const uint64_t* __restrict__ ptrs, int ptr_stride,
+                                                const uint32_t* __restrict__ tbl, const uint64_t* __restrict__ ltg,
+                                                int len, int k, unsigned nitems, unsigned tiles) {
+  ldsx_items<P, 2, kBufNT, 128>(ptrs, ptr_stride, 0, k, tbl, ltg, len, k, nitems, tiles);
+}
+
+// lanes mode: ec_encode_ldsx<P, 2> at 256 lanes against ldsx_items at 128 lanes
+// under dynamic-LDS occupancy caps (0 = its tables only), bench.py's layout.
+static int lanes_main(int iters, int rounds) {
+  struct Sh { int k, p, len, ns; };
+  const Sh shapes[] = {{20, 8, 4 << 20, 64}, {20, 6, 4 << 20, 64}, {16, 8, 1 << 20, 512}, {10, 8, 1 << 20, 1024}};
+  // LANES_ORDER=1: 256 lanes only, cap 0 measured first and last (is the first
+  // configuration of a shape slow only because it runs first?)
+  const bool order = getenv("LANES_ORDER") != nullptr;
+  const std::vector<int> caps = order ? std::vector<int>{0, 16384, 20480, 0, 16384, 0}
+                                      : std::vector<int>{0, 8192, 10240, 13312, 16384, 20480};
+  const std::vector<int> lane_set = order ? std::vector<int>{256} : std::vector<int>{256, 128};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int round = 0; round < rounds; ++round)
+    for (const Sh& sh : shapes) {
+      const int k = sh.k, p = sh.p, len = sh.len, ns = sh.ns, stride = k + p;
+      const size_t shard = static_cast<size_t>(len);
+      uint8_t *d = nullptr, *c = nullptr;
+      CK(hipMalloc(&d, shard * k * ns));
+      CK(hipMalloc(&c, shard * p * ns));
+      hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t*>(d), shard * k * ns / 8, 5ull + k);
+      std::vector<uint64_t> hp(static_cast<size_t>(stride) * ns);
+      for (int st = 0; st < ns; ++st)
+        for (int i = 0; i < stride; ++i)
+          hp[static_cast<size_t>(st) * stride + i] = reinterpret_cast<uint64_t>(
+              i < k ? d + (static_cast<size_t>(st) * k + i) * shard : c + (static_cast<size_t>(st) * p + i - k) * shard);
+      uint64_t* dp = nullptr;
+      CK(hipMalloc(&dp, hp.size() * 8));
+      CK(hipMemcpy(dp, hp.data(), hp.size() * 8, hipMemcpyHostToDevice));
+      std::vector<unsigned char> a(stride * k), g(32 * k * p);
+      gf_gen_rs_matrix(a.data(), stride, k);
+      ec_init_tables(k, p, a.data() + k * k, g.data());
+      std::vector<uint32_t> ht(isal_hip_tables_dwords(k, p) + 1);
+      isal_hip_build_tables(k, p, g.data(), ht.data());
+      uint32_t* dt = nullptr;
+      CK(hipMalloc(&dt, ht.size() * 4));
+      CK(hipMemcpy(dt, ht.data(), ht.size() * 4, hipMemcpyHostToDevice));
+      std::vector<uint64_t> hl(isal_hip_ldsx_words(k, p));
+      isal_hip_build_ldsx_tables(k, p, g.data(), hl.data());
+      uint64_t* dl = nullptr;
+      CK(hipMalloc(&dl, hl.size() * 8));
+      CK(hipMemcpy(dl, hl.data(), hl.size() * 8, hipMemcpyHostToDevice));
+      const size_t lt = static_cast<size_t>(k) * ISAL_HIP_LDSX_ENTRIES * 8;
+      const uint8_t* last = c + static_cast<size_t>(ns - 1) * p * shard;
+      std::vector<uint8_t> ref(shard * p), got(shard * p);
+      const unsigned t256 = len / kTile, t128 = len / (128 * kVec);
+      auto run = [&](int lanes, int cap) {
+        const size_t dyn = lt > static_cast<size_t>(cap) ? lt : static_cast<size_t>(cap);
+        if (lanes == 256) {
+          if (p == 8)
+            hipLaunchKernelGGL((ec_encode_ldsx<8, 2>), dim3(t256 * ns), dim3(256), dyn, 0, dp, stride, 0, k, dt, dl, len,
+                               k, t256 * ns, t256);
+          else
+            hipLaunchKernelGGL((ec_encode_ldsx<6, 2>), dim3(t256 * ns), dim3(256), dyn, 0, dp, stride, 0, k, dt, dl, len,
+                               k, t256 * ns, t256);
+        } else {
+          if (p == 8)
+            hipLaunchKernelGGL((ldsx_128<8>), dim3(t128 * ns), dim3(128), dyn, 0, dp, stride, dt, dl, len, k, t128 * ns,
+                               t128);
+          else
+            hipLaunchKernelGGL((ldsx_128<6>), dim3(t128 * ns), dim3(128), dyn, 0, dp, stride, dt, dl, len, k, t128 * ns,
+                               t128);
+        }
+      };
+      run(256, 0);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(ref.data(), last, shard * p, hipMemcpyDeviceToHost));
+      for (int lanes : lane_set)
+        for (int cap : caps) {
+          CK(hipMemset(const_cast<uint8_t*>(last), 0xA5, shard * p));
+          run(lanes, cap);
+          CK(hipDeviceSynchronize());
+          CK(hipGetLastError());
+          CK(hipMemcpy(got.data(), last, shard * p, hipMemcpyDeviceToHost));
+          const bool ok = memcmp(ref.data(), got.data(), shard * p) == 0;
+          for (int w = 0; w < 2; ++w) run(lanes, cap);
+          CK(hipEventRecord(e0, 0));
+          for (int it = 0; it < iters; ++it) run(lanes, cap);
+          CK(hipEventRecord(e1, 0));
+          CK(hipEventSynchronize(e1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          ms /= iters;
+          const double bytes = static_cast<double>(stride) * shard * ns;
+          printf("{\"round\": %d, \"k\": %d, \"p\": %d, \"lanes\": %d, \"cap\": %d, \"ms\": %.4f, \"frac\": %.4f, "
+                 "\"bit_exact\": %s}\n", round, k, p, lanes, cap, ms, bytes / ms / 1e6 / 8000.0, ok ? "true" : "false");
+          fflush(stdout);
+        }
+      CK(hipFree(d));
+      CK(hipFree(c));
+      CK(hipFree(dp));
+      CK(hipFree(dt));
+      CK(hipFree(dl));
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 10;
+  if (argc > 4 && strcmp(argv[4], "lanes") == 0) return lanes_main(iters, argc > 2 ? atoi(argv[2]) : 1);
   if (argc > 4 && strcmp(argv[4], "matrix") == 0)
     return matrix_main(iters, argc > 2 ? atoi(argv[2]) : 1, argc > 3 ? atoi(argv[3]) : 1);
   const int rounds = argc > 2 ? atoi(argv[2]) : 2;
